@@ -1,0 +1,154 @@
+/*
+ * lsmgpu.h -- C ABI of the MI355X-native (gfx950 / CDNA4) SST block codec for lsmdb.
+ *
+ * This is the drop-in boundary.  The reference (impact-eintr/lsmdb @ v0, pure Go) has no FFI
+ * layer: the path sits behind the Go `table` package.  Each entry point below names the
+ * reference interface it replaces (file:line); INTEGRATION.md shows the cgo shim that binds
+ * them so table.Builder / table.Table keep their Go API and the on-disk .sst layout.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only; the caller owns every buffer; nothing is retained past
+ *    return (cgo pointer rules).  `*_on_device` flags say whether pointers are HIP device
+ *    pointers (device-resident path) or host pointers (the library stages through HBM).
+ *  - Offsets inside one call are u32, as in the SST format itself (builder.go:53,146-160);
+ *    one call handles at most 4 GiB - 1 of block bytes.
+ *  - Functions return LSMGPU_OK (0) or a positive LSMGPU_ERR_* code; they never abort.
+ *  - One lsmgpu_ctx per OS thread (like a Go Builder/Iterator: single-goroutine objects).
+ */
+#ifndef LSMGPU_H
+#define LSMGPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LSMGPU_ABI_VERSION 1
+
+/* ---- call status ---- */
+#define LSMGPU_OK 0
+#define LSMGPU_ERR_ARG 1        /* NULL / inconsistent argument                               */
+#define LSMGPU_ERR_BAD_TAIL 2   /* malformed SST tail: table.go:177-215 would panic or ErrEOF  */
+#define LSMGPU_ERR_CAPACITY 3   /* an output buffer is too small; lsmgpu_decoded.* has the need */
+#define LSMGPU_ERR_HIP 4        /* HIP runtime error                                          */
+#define LSMGPU_ERR_KEY_LEN 5    /* encode: key length <= 8 (y.go:98 AssertTruef) or > 65535    */
+#define LSMGPU_ERR_VALUE_LEN 6  /* encode: vs-enc > 65535 (y/iterator.go:31-38 uint16 trunc.) */
+#define LSMGPU_ERR_TOO_LARGE 7  /* more than 4 GiB - 1 bytes in one call                        */
+#define LSMGPU_ERR_INTERNAL 8   /* device look-back did not converge (never expected)          */
+#define LSMGPU_ERR_NO_DEVICE 9  /* no HIP device / bad device index                            */
+
+/* ---- per-block decode status (lsmgpu_decoded.blk_status) ---- */
+#define LSMGPU_BLK_OK 0             /* terminator, or pos >= len (iterator.go:115-118,124-127) */
+#define LSMGPU_BLK_VALUE_OVERFLOW 1 /* "Value exceeded size of block" (iterator.go:103-106)     */
+#define LSMGPU_BLK_FIRST_PLEN 2     /* AssertTrue(h.plen == 0) (iterator.go:131, table.go:239)  */
+#define LSMGPU_BLK_TRUNC_HEADER 3   /* < 10 B left for a header (Go reads past the block slice)  */
+#define LSMGPU_BLK_PREFIX_OOB 4     /* baseKey[:plen] would read past the block                 */
+#define LSMGPU_BLK_RANGE 5          /* block [off, off+len) is outside the data buffer          */
+
+/* ---- decode modes (bit mask) ---- */
+#define LSMGPU_MODE_MATERIALIZE 1 /* key_data/key_end + val_data/val_end                       */
+#define LSMGPU_MODE_VIEW 2        /* view[] zero-copy entry index                              */
+
+typedef struct lsmgpu_ctx lsmgpu_ctx;
+
+/* Context: owns a HIP stream (or borrows one), look-back scratch and staging buffers. */
+int lsmgpu_open(int device, lsmgpu_ctx** out);
+void lsmgpu_close(lsmgpu_ctx* ctx);
+/* Use an external hipStream_t (e.g. the caller's current stream); NULL restores the ctx's own. */
+int lsmgpu_set_stream(lsmgpu_ctx* ctx, void* hip_stream);
+void* lsmgpu_get_stream(lsmgpu_ctx* ctx);
+int lsmgpu_synchronize(lsmgpu_ctx* ctx);
+const char* lsmgpu_strerror(int code);
+int lsmgpu_abi_version(void);
+
+/* Replaces Table.readIndex's tail parse (table/table.go:177-215): bloom length + bloom span,
+ * restart count, restart offsets -> block b = [blk_off[b], blk_off[b]+blk_len[b]).  Host only.
+ * *nblk is set even when cap is too small (then LSMGPU_ERR_CAPACITY). */
+int lsmgpu_parse_index(const uint8_t* sst, uint64_t len, uint32_t* blk_off, uint32_t* blk_len,
+                       uint64_t cap, uint64_t* nblk, uint64_t* bloom_off, uint64_t* bloom_len);
+
+/* Decoded output.  In materialize mode, entry i (in Table.Iterator order) has
+ *   key   = key_data[key_end[i-1] : key_end[i]]   (blockIterator.Key(): baseKey[:plen] ++ diff)
+ *   value = val_data[val_end[i-1] : val_end[i]]   (blockIterator.Value(): raw ValueStruct bytes)
+ * (key_end[-1] = val_end[-1] = 0).  In view mode view[i] = key_pos | klen << 32 | vlen << 48
+ * where key_pos is the absolute offset of the entry's stored key bytes in `data` (header at
+ * key_pos-10, value at key_pos+klen).  blk_first[b] = first entry of block b (nblk+1 words),
+ * blk_status[b] = LSMGPU_BLK_*.  Entries of a block with an error status are the ones the Go
+ * blockIterator yields before it turns invalid. */
+typedef struct {
+  uint8_t* key_data;  uint64_t key_cap;
+  uint32_t* key_end;
+  uint8_t* val_data;  uint64_t val_cap;
+  uint32_t* val_end;
+  uint64_t* view;
+  uint64_t ent_cap;          /* capacity (entries) of key_end / val_end / view */
+  uint32_t* blk_first;       /* nblk + 1 */
+  int32_t* blk_status;       /* nblk */
+  /* results, written by the synchronous call */
+  uint64_t n_entries, key_bytes, val_bytes;
+  int64_t first_bad_block;   /* -1 if every block decoded cleanly */
+  uint64_t n_bad_blocks;
+} lsmgpu_decoded;
+
+/* Replaces the per-entry blockIterator.Next/parseKV loop (table/iterator.go:93-135) driven by
+ * Iterator.seekToFirst/next (iterator.go:201-217,301-326) over a batch of blocks, e.g. every
+ * block of the tables compactBuildTables (levels.go:239-338) merges.  blk_off/blk_len are host
+ * arrays (from lsmgpu_parse_index, offsets relative to `data`).  If data_on_device is 0, `data`
+ * and every output pointer are host memory and the library stages through HBM. */
+int lsmgpu_decode_blocks(lsmgpu_ctx* ctx, const uint8_t* data, uint64_t data_len,
+                         int data_on_device, const uint32_t* blk_off, const uint32_t* blk_len,
+                         uint64_t nblk, int mode, lsmgpu_decoded* out);
+
+/* Device-resident asynchronous form (the benchmarked kernel): all pointers are device
+ * pointers, max_blk_len bounds blk_len[] (selects the LDS slot), `d_result` (device, 8 u64)
+ * receives {n_entries, key_bytes, val_bytes, first_bad_block+1, n_bad_blocks, flags, 0, 0}
+ * with flags bit0 = capacity overflow, bit1 = look-back timeout.  Enqueued on the ctx stream. */
+int lsmgpu_decode_blocks_async(lsmgpu_ctx* ctx, const uint8_t* d_data, uint64_t data_len,
+                               const uint32_t* d_blk_off, const uint32_t* d_blk_len,
+                               uint64_t nblk, uint32_t max_blk_len, int mode,
+                               const lsmgpu_decoded* out, uint64_t* d_result);
+
+/* Replaces Builder.Add x n + Builder.Finish minus the bloom (table/builder.go:84-198):
+ * entry i = (keys[key_end[i-1]:key_end[i]], vs[vs_end[i-1]:vs_end[i]]) where vs is the
+ * encoded ValueStruct (y/iterator.go:48-62), entries sorted by the caller as Add requires.
+ * Blocks are cut every entries_per_block entries (resultInterval, builder.go:14,126; 100 is the
+ * reference) or, if block_bytes > 0, before an entry that would grow a non-empty block past
+ * block_bytes (opt-in knob, not in the reference).  Writes [data blocks][restarts BE32 x N]
+ * [N BE32] to out; the caller appends bbloom JSON + BE32(len) exactly as builder.go:190-195.
+ * restarts (host, optional) receives the block end offsets. */
+int lsmgpu_encode_blocks(lsmgpu_ctx* ctx, const uint8_t* keys, const uint32_t* key_end,
+                         const uint8_t* vs, const uint32_t* vs_end, uint64_t n, int on_device,
+                         uint32_t entries_per_block, uint32_t block_bytes, uint8_t* out,
+                         uint64_t out_cap, uint64_t* out_len, uint64_t* data_len,
+                         uint32_t* restarts, uint64_t restarts_cap, uint64_t* nrestarts);
+
+/* Device-resident asynchronous encode with a precomputed block plan: d_blk_first (device,
+ * nblocks+1 entry indices) or NULL with entries_per_block > 0.  key_total/vs_total are
+ * key_end[n-1]/vs_end[n-1].  d_flags (device u32) gets bit0 = key length error,
+ * bit1 = value length error.  Output length = 10n + key_total + vs_total + 13*nblocks
+ * + 4*nblocks + 4. */
+int lsmgpu_encode_blocks_async(lsmgpu_ctx* ctx, const uint8_t* d_keys, const uint32_t* d_key_end,
+                               const uint8_t* d_vs, const uint32_t* d_vs_end, uint64_t n,
+                               uint32_t entries_per_block, const uint32_t* d_blk_first,
+                               uint64_t nblocks, uint64_t key_total, uint64_t vs_total,
+                               uint8_t* d_out, uint64_t out_cap, uint32_t* d_flags);
+
+/* Host block planner for the byte-target policy (same rule as lsmgpu_encode_blocks).
+ * Writes blk_first[0..nblocks] (cap entries) and returns the block count in *nblocks. */
+int lsmgpu_plan_blocks(const uint32_t* key_end, const uint32_t* vs_end, uint64_t n,
+                       uint32_t entries_per_block, uint32_t block_bytes, uint32_t* blk_first,
+                       uint64_t cap, uint64_t* nblocks);
+
+/* Replaces ValueStruct.EncodeTo (y/iterator.go:55-62) for a batch of values:
+ * vs[i] = [meta[i]][user_meta[i]][uvarint expires_at[i]][values[value_end[i-1]:value_end[i]]].
+ * vs_end (n words) receives running end offsets.  on_device selects pointer space. */
+int lsmgpu_encode_values(lsmgpu_ctx* ctx, const uint8_t* meta, const uint8_t* user_meta,
+                         const uint64_t* expires_at, const uint8_t* values,
+                         const uint32_t* value_end, uint64_t n, int on_device, uint8_t* vs,
+                         uint64_t vs_cap, uint32_t* vs_end, uint64_t* vs_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LSMGPU_H */

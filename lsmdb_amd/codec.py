@@ -1,0 +1,291 @@
+"""Python face of the HIP SST block codec (C ABI: include/lsmgpu.h).
+
+`Codec` owns one `lsmgpu_ctx` (HIP stream + look-back scratch) on one device.  Two families:
+
+* host-buffer calls (`decode_host`, `encode_host`, `encode_values_host`): the library stages
+  through HBM -- the path a cgo caller with an mmap'd .sst takes;
+* device-resident calls (`decode_device_async`, `encode_device_async`): every pointer is a
+  torch CUDA tensor; nothing is synchronised (what bench.py times).
+
+No CPU fallback exists: every call runs the gfx950 kernels or raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_uint64, c_void_p
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import (LsmgpuDecoded, LsmgpuError, MODE_MATERIALIZE, MODE_VIEW, check, lib)
+
+
+def _ptr(a) -> Optional[int]:
+    """Address of a numpy array / torch tensor / bytes-like (None passes through)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data if a.size else (a.ctypes.data or None)
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr() or None
+    raise TypeError(f"unsupported buffer type {type(a)}")
+
+
+def _np_u8(data) -> np.ndarray:
+    if isinstance(data, np.ndarray):
+        return np.ascontiguousarray(data.view(np.uint8).reshape(-1))
+    return np.frombuffer(memoryview(data), dtype=np.uint8)
+
+
+# ------------------------------------------------------------------ table.go:177-215
+def parse_index(sst) -> tuple[np.ndarray, np.ndarray, int, int]:
+    """Table.readIndex's tail parse: returns (blk_off, blk_len, bloom_off, bloom_len)."""
+    buf = _np_u8(sst)
+    n = c_uint64(0)
+    bo, bl = c_uint64(0), c_uint64(0)
+    rc = lib().lsmgpu_parse_index(_ptr(buf), buf.size, None, None, 0, byref(n), byref(bo), byref(bl))
+    if rc not in (_lib.OK, _lib.ERR_CAPACITY):
+        raise LsmgpuError(rc, "parse_index")
+    off = np.zeros(max(n.value, 1), dtype=np.uint32)
+    ln = np.zeros(max(n.value, 1), dtype=np.uint32)
+    check(lib().lsmgpu_parse_index(_ptr(buf), buf.size, _ptr(off), _ptr(ln), off.size, byref(n),
+                                   byref(bo), byref(bl)), "parse_index")
+    return off[: n.value], ln[: n.value], bo.value, bl.value
+
+
+def plan_blocks(key_end: np.ndarray, vs_end: np.ndarray, entries_per_block: int = 100,
+                block_bytes: int = 0) -> np.ndarray:
+    """Block plan (first entry of each block + end sentinel) of Builder.Add's cut rule."""
+    ke = np.ascontiguousarray(key_end, dtype=np.uint32)
+    ve = np.ascontiguousarray(vs_end, dtype=np.uint32)
+    nb = c_uint64(0)
+    check(lib().lsmgpu_plan_blocks(_ptr(ke), _ptr(ve), ke.size, entries_per_block, block_bytes,
+                                   None, 0, byref(nb)), "plan_blocks")
+    out = np.zeros(nb.value + 1, dtype=np.uint32)
+    check(lib().lsmgpu_plan_blocks(_ptr(ke), _ptr(ve), ke.size, entries_per_block, block_bytes,
+                                   _ptr(out), out.size, byref(nb)), "plan_blocks")
+    return out
+
+
+@dataclass
+class HostDecoded:
+    """A decoded batch in host memory (SoA, Table.Iterator order)."""
+    n_entries: int
+    key_data: np.ndarray
+    key_end: np.ndarray
+    val_data: np.ndarray
+    val_end: np.ndarray
+    view: Optional[np.ndarray]
+    blk_first: np.ndarray
+    blk_status: np.ndarray
+    first_bad_block: int
+    n_bad_blocks: int
+
+    def key(self, i: int) -> bytes:
+        a = int(self.key_end[i - 1]) if i else 0
+        return self.key_data[a: int(self.key_end[i])].tobytes()
+
+    def value(self, i: int) -> bytes:
+        a = int(self.val_end[i - 1]) if i else 0
+        return self.val_data[a: int(self.val_end[i])].tobytes()
+
+
+@dataclass
+class DeviceDecodeBuffers:
+    """Device output buffers of a decode (torch CUDA tensors); built by Codec.alloc_decode."""
+    key_data: object = None
+    key_end: object = None
+    val_data: object = None
+    val_end: object = None
+    view: object = None
+    blk_first: object = None
+    blk_status: object = None
+    result: object = None
+    ent_cap: int = 0
+    struct: LsmgpuDecoded = field(default_factory=LsmgpuDecoded)
+
+    def bind(self) -> LsmgpuDecoded:
+        s = self.struct
+        s.key_data = _ptr(self.key_data)
+        s.key_cap = self.key_data.numel() if self.key_data is not None else 0
+        s.key_end = _ptr(self.key_end)
+        s.val_data = _ptr(self.val_data)
+        s.val_cap = self.val_data.numel() if self.val_data is not None else 0
+        s.val_end = _ptr(self.val_end)
+        s.view = _ptr(self.view)
+        s.ent_cap = self.ent_cap
+        s.blk_first = _ptr(self.blk_first)
+        s.blk_status = _ptr(self.blk_status)
+        return s
+
+
+class Codec:
+    """One lsmgpu_ctx on one HIP device (use one per thread, like a Go Builder/Iterator)."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        self._ctx = c_void_p()
+        check(lib().lsmgpu_open(device, byref(self._ctx)), f"lsmgpu_open({device})")
+
+    # -- lifecycle
+    def close(self) -> None:
+        if self._ctx:
+            lib().lsmgpu_close(self._ctx)
+            self._ctx = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def set_stream(self, stream_handle: Optional[int]) -> None:
+        check(lib().lsmgpu_set_stream(self._ctx, stream_handle), "set_stream")
+
+    def stream_handle(self) -> int:
+        return lib().lsmgpu_get_stream(self._ctx) or 0
+
+    def synchronize(self) -> None:
+        check(lib().lsmgpu_synchronize(self._ctx), "synchronize")
+
+    # -- decode, host buffers (table.Table path)
+    def decode_host(self, data, blk_off: np.ndarray, blk_len: np.ndarray,
+                    mode: int = MODE_MATERIALIZE | MODE_VIEW) -> HostDecoded:
+        buf = _np_u8(data)
+        off = np.ascontiguousarray(blk_off, dtype=np.uint32)
+        ln = np.ascontiguousarray(blk_len, dtype=np.uint32)
+        nblk = off.size
+        key_cap = val_cap = max(int(buf.size), 16)
+        ent_cap = max(int(ln.astype(np.uint64).sum()) // 10 + 1, 1)
+        for _attempt in range(2):
+            kd = np.zeros(key_cap, dtype=np.uint8)
+            vd = np.zeros(val_cap, dtype=np.uint8)
+            ke = np.zeros(ent_cap, dtype=np.uint32)
+            ve = np.zeros(ent_cap, dtype=np.uint32)
+            vw = np.zeros(ent_cap, dtype=np.uint64) if mode & MODE_VIEW else None
+            bf = np.zeros(nblk + 1, dtype=np.uint32)
+            bs = np.zeros(max(nblk, 1), dtype=np.int32)
+            d = LsmgpuDecoded()
+            d.key_data, d.key_cap, d.key_end = _ptr(kd), kd.size, _ptr(ke)
+            d.val_data, d.val_cap, d.val_end = _ptr(vd), vd.size, _ptr(ve)
+            d.view, d.ent_cap = _ptr(vw), ent_cap
+            d.blk_first, d.blk_status = _ptr(bf), _ptr(bs)
+            rc = lib().lsmgpu_decode_blocks(self._ctx, _ptr(buf), buf.size, 0, _ptr(off), _ptr(ln),
+                                            nblk, mode | MODE_MATERIALIZE, byref(d))
+            if rc == _lib.ERR_CAPACITY:  # plen>0 blocks can expand keys: retry with exact sizes
+                key_cap = max(int(d.key_bytes), 16)
+                val_cap = max(int(d.val_bytes), 16)
+                ent_cap = max(int(d.n_entries), 1)
+                continue
+            check(rc, "decode_blocks")
+            n = int(d.n_entries)
+            return HostDecoded(n, kd[: d.key_bytes], ke[:n], vd[: d.val_bytes], ve[:n],
+                               vw[:n] if vw is not None else None, bf, bs[:nblk],
+                               int(d.first_bad_block), int(d.n_bad_blocks))
+        raise LsmgpuError(_lib.ERR_CAPACITY, "decode_blocks")
+
+    # -- decode, device-resident (benchmarked path)
+    def alloc_decode(self, data_len: int, total_block_bytes: int, nblk: int, mode: int,
+                     ent_cap: Optional[int] = None):
+        import torch
+        dev = torch.device("cuda", self.device)
+        ent_cap = ent_cap if ent_cap is not None else total_block_bytes // 10 + 1
+        b = DeviceDecodeBuffers(ent_cap=ent_cap)
+        if mode & MODE_MATERIALIZE:
+            b.key_data = torch.empty(max(total_block_bytes, 16), dtype=torch.uint8, device=dev)
+            b.val_data = torch.empty(max(total_block_bytes, 16), dtype=torch.uint8, device=dev)
+            b.key_end = torch.empty(ent_cap, dtype=torch.int32, device=dev)
+            b.val_end = torch.empty(ent_cap, dtype=torch.int32, device=dev)
+        if mode & MODE_VIEW:
+            b.view = torch.empty(ent_cap, dtype=torch.int64, device=dev)
+        b.blk_first = torch.empty(nblk + 1, dtype=torch.int32, device=dev)
+        b.blk_status = torch.empty(max(nblk, 1), dtype=torch.int32, device=dev)
+        b.result = torch.zeros(8, dtype=torch.int64, device=dev)
+        b.bind()
+        return b
+
+    def decode_device_async(self, data, blk_off, blk_len, max_blk_len: int, mode: int,
+                            bufs: DeviceDecodeBuffers, data_len: Optional[int] = None) -> None:
+        n = blk_off.numel()
+        dl = data.numel() if data_len is None else data_len
+        check(lib().lsmgpu_decode_blocks_async(self._ctx, _ptr(data), dl, _ptr(blk_off),
+                                               _ptr(blk_len), n, max_blk_len, mode,
+                                               byref(bufs.struct), _ptr(bufs.result)),
+              "decode_blocks_async")
+
+    # -- encode
+    def encode_host(self, keys, key_end, vs, vs_end, entries_per_block: int = 100,
+                    block_bytes: int = 0):
+        """Builder.Add x n + Finish (minus bloom): returns (sst_without_bloom, data_len, restarts)."""
+        kb = _np_u8(keys) if len(keys) else np.zeros(1, np.uint8)
+        vb = _np_u8(vs) if len(vs) else np.zeros(1, np.uint8)
+        ke = np.ascontiguousarray(key_end, dtype=np.uint32)
+        ve = np.ascontiguousarray(vs_end, dtype=np.uint32)
+        n = ke.size
+        out_len, data_len, nr = c_uint64(0), c_uint64(0), c_uint64(0)
+        rc = lib().lsmgpu_encode_blocks(self._ctx, _ptr(kb), _ptr(ke), _ptr(vb), _ptr(ve), n, 0,
+                                        entries_per_block, block_bytes, _ptr(np.zeros(1, np.uint8)),
+                                        0, byref(out_len), byref(data_len), None, 0, byref(nr))
+        if rc != _lib.ERR_CAPACITY:
+            check(rc, "encode_blocks")
+        out = np.zeros(out_len.value, dtype=np.uint8)
+        rs = np.zeros(max(nr.value, 1), dtype=np.uint32)
+        check(lib().lsmgpu_encode_blocks(self._ctx, _ptr(kb), _ptr(ke), _ptr(vb), _ptr(ve), n, 0,
+                                         entries_per_block, block_bytes, _ptr(out), out.size,
+                                         byref(out_len), byref(data_len), _ptr(rs), rs.size,
+                                         byref(nr)), "encode_blocks")
+        return out.tobytes(), int(data_len.value), rs[: nr.value]
+
+    def encode_device_async(self, keys, key_end, vs, vs_end, n: int, key_total: int,
+                            vs_total: int, out, flags, entries_per_block: int = 100,
+                            blk_first=None, nblocks: int = 0) -> None:
+        check(lib().lsmgpu_encode_blocks_async(self._ctx, _ptr(keys), _ptr(key_end), _ptr(vs),
+                                               _ptr(vs_end), n, entries_per_block,
+                                               _ptr(blk_first), nblocks, key_total, vs_total,
+                                               _ptr(out), out.numel(), _ptr(flags)),
+              "encode_blocks_async")
+
+    def encode_values_host(self, meta, user_meta, expires_at, values, value_end):
+        """ValueStruct.EncodeTo for a batch: returns (vs bytes, vs_end)."""
+        m = np.ascontiguousarray(meta, dtype=np.uint8)
+        um = np.ascontiguousarray(user_meta, dtype=np.uint8)
+        ex = np.ascontiguousarray(expires_at, dtype=np.uint64)
+        vb = _np_u8(values) if len(values) else np.zeros(1, np.uint8)
+        ve = np.ascontiguousarray(value_end, dtype=np.uint32)
+        n = m.size
+        if n == 0:
+            return b"", np.zeros(0, np.uint32)
+        cap = int(ve[-1]) + 12 * n + 16
+        out = np.zeros(cap, dtype=np.uint8)
+        end = np.zeros(n, dtype=np.uint32)
+        ln = c_uint64(0)
+        check(lib().lsmgpu_encode_values(self._ctx, _ptr(m), _ptr(um), _ptr(ex), _ptr(vb), _ptr(ve),
+                                         n, 0, _ptr(out), out.size, _ptr(end), byref(ln)),
+              "encode_values")
+        return out[: ln.value].tobytes(), end
+
+
+_DEFAULT: dict[int, Codec] = {}
+
+
+def default_codec(device: Optional[int] = None) -> Codec:
+    """Process-wide Codec per device (lazily opened)."""
+    if device is None:
+        device = 0
+    c = _DEFAULT.get(device)
+    if c is None:
+        c = _DEFAULT[device] = Codec(device)
+    return c
+
+
+__all__ = ["Codec", "HostDecoded", "DeviceDecodeBuffers", "parse_index", "plan_blocks",
+           "default_codec", "MODE_MATERIALIZE", "MODE_VIEW"]
+_ = ctypes

@@ -1,0 +1,546 @@
+// api.hip -- the C ABI (include/lsmgpu.h) over the gfx950 codec kernels.
+// Host-side responsibilities: argument validation, the SST tail parse (table.go:177-215),
+// staging of host buffers through HBM, look-back scratch / epoch tags, block planning.
+#include <hip/hip_runtime.h>
+#include <rocprim/device/device_scan.hpp>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/lsmgpu.h"
+#include "kernels.hpp"
+
+using namespace lsmgpu;
+
+namespace {
+
+constexpr uint32_t kTagMax = (1u << 24) - 1;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t need) {
+    if (need <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t n = std::max<size_t>(need, 256);
+    hipError_t e = hipMalloc(&p, n);
+    if (e == hipSuccess) cap = n;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+inline uint32_t rd_be32(const uint8_t* b) {
+  return ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
+}
+
+}  // namespace
+
+struct lsmgpu_ctx {
+  int device = 0;
+  int num_cus = 256;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  DevBuf lb;             // look-back granules (64 B per block)
+  DevBuf ticket;         // u64 monotonic ticket counter
+  uint64_t ticket_val = 0;
+  DevBuf result;         // 8 x u64
+  uint64_t* h_result = nullptr;  // pinned
+  uint32_t tag = 0;
+  DevBuf flags;          // encode flags
+  DevBuf scan_tmp;
+  // staging for host-memory calls
+  DevBuf s_data, s_off, s_len, s_kd, s_ke, s_vd, s_ve, s_view, s_bf, s_bs, s_a, s_b, s_c, s_d;
+};
+
+#define HIPC(x)                                   \
+  do {                                            \
+    hipError_t _e = (x);                          \
+    if (_e != hipSuccess) return LSMGPU_ERR_HIP;  \
+  } while (0)
+
+extern "C" {
+
+int lsmgpu_abi_version(void) { return LSMGPU_ABI_VERSION; }
+
+const char* lsmgpu_strerror(int code) {
+  switch (code) {
+    case LSMGPU_OK: return "ok";
+    case LSMGPU_ERR_ARG: return "invalid argument";
+    case LSMGPU_ERR_BAD_TAIL: return "malformed SST index tail";
+    case LSMGPU_ERR_CAPACITY: return "output buffer too small";
+    case LSMGPU_ERR_HIP: return "HIP runtime error";
+    case LSMGPU_ERR_KEY_LEN: return "key length must be in (8, 65535]";
+    case LSMGPU_ERR_VALUE_LEN: return "encoded value longer than 65535 bytes";
+    case LSMGPU_ERR_TOO_LARGE: return "more than 4 GiB - 1 bytes in one call";
+    case LSMGPU_ERR_INTERNAL: return "device look-back did not converge";
+    case LSMGPU_ERR_NO_DEVICE: return "no HIP device";
+    default: return "unknown error";
+  }
+}
+
+int lsmgpu_open(int device, lsmgpu_ctx** out) {
+  if (!out) return LSMGPU_ERR_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return LSMGPU_ERR_NO_DEVICE;
+  if (device < 0 || device >= ndev) return LSMGPU_ERR_NO_DEVICE;
+  HIPC(hipSetDevice(device));
+  lsmgpu_ctx* c = new lsmgpu_ctx();
+  c->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    c->num_cus = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return LSMGPU_ERR_HIP;
+  }
+  c->stream = c->own_stream;
+  if (c->ticket.ensure(64) != hipSuccess || c->result.ensure(64) != hipSuccess ||
+      c->flags.ensure(64) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&c->h_result), 64, hipHostMallocDefault) != hipSuccess ||
+      hipMemset(c->ticket.p, 0, 64) != hipSuccess) {
+    lsmgpu_close(c);
+    return LSMGPU_ERR_HIP;
+  }
+  c->ticket_val = 0;
+  *out = c;
+  return LSMGPU_OK;
+}
+
+void lsmgpu_close(lsmgpu_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+  DevBuf* bufs[] = {&c->lb, &c->ticket, &c->result, &c->flags, &c->scan_tmp, &c->s_data,
+                    &c->s_off, &c->s_len, &c->s_kd, &c->s_ke, &c->s_vd, &c->s_ve, &c->s_view,
+                    &c->s_bf, &c->s_bs, &c->s_a, &c->s_b, &c->s_c, &c->s_d};
+  for (DevBuf* b : bufs) b->release();
+  if (c->h_result) (void)hipHostFree(c->h_result);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+}
+
+int lsmgpu_set_stream(lsmgpu_ctx* c, void* s) {
+  if (!c) return LSMGPU_ERR_ARG;
+  c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own_stream;
+  return LSMGPU_OK;
+}
+
+void* lsmgpu_get_stream(lsmgpu_ctx* c) { return c ? reinterpret_cast<void*>(c->stream) : nullptr; }
+
+int lsmgpu_synchronize(lsmgpu_ctx* c) {
+  if (!c) return LSMGPU_ERR_ARG;
+  HIPC(hipStreamSynchronize(c->stream));
+  return LSMGPU_OK;
+}
+
+// ------------------------------------------------------------------ index (table.go:177-215)
+int lsmgpu_parse_index(const uint8_t* sst, uint64_t len, uint32_t* blk_off, uint32_t* blk_len,
+                       uint64_t cap, uint64_t* nblk, uint64_t* bloom_off, uint64_t* bloom_len) {
+  if (!sst || !nblk) return LSMGPU_ERR_ARG;
+  *nblk = 0;
+  if (len < 8) return LSMGPU_ERR_BAD_TAIL;
+  uint64_t pos = len - 4;
+  uint32_t bl = rd_be32(sst + pos);                    // table.go:181-183
+  if (bl > pos || pos - bl < 4) return LSMGPU_ERR_BAD_TAIL;
+  pos -= bl;
+  if (bloom_off) *bloom_off = pos;
+  if (bloom_len) *bloom_len = bl;
+  pos -= 4;                                            // table.go:188-190
+  uint32_t nr = rd_be32(sst + pos);
+  if ((uint64_t)nr * 4 > pos) return LSMGPU_ERR_BAD_TAIL;
+  pos -= (uint64_t)nr * 4;                             // table.go:192-199
+  *nblk = nr;
+  if (nr > cap || (nr && (!blk_off || !blk_len))) return LSMGPU_ERR_CAPACITY;
+  uint32_t prev = 0;
+  for (uint32_t i = 0; i < nr; i++) {                  // table.go:202-215
+    uint32_t o = rd_be32(sst + pos + 4ull * i);
+    if (o < prev || (uint64_t)o > pos) return LSMGPU_ERR_BAD_TAIL;
+    blk_off[i] = prev;
+    blk_len[i] = o - prev;
+    prev = o;
+  }
+  return LSMGPU_OK;
+}
+
+// ------------------------------------------------------------------ decode
+static void next_tag(lsmgpu_ctx* c, uint64_t nblk) {
+  if (c->tag >= kTagMax) {  // epoch wrap: clear every granule so stale tags cannot match
+    (void)hipMemsetAsync(c->lb.p, 0, c->lb.cap, c->stream);
+    c->tag = 0;
+  }
+  c->tag++;
+  (void)nblk;
+}
+
+int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t data_len,
+                               const uint32_t* d_blk_off, const uint32_t* d_blk_len,
+                               uint64_t nblk, uint32_t max_blk_len, int mode,
+                               const lsmgpu_decoded* out, uint64_t* d_result) {
+  if (!c || !out || !d_result) return LSMGPU_ERR_ARG;
+  if (mode & ~(LSMGPU_MODE_MATERIALIZE | LSMGPU_MODE_VIEW)) return LSMGPU_ERR_ARG;
+  if (data_len > 0xffffffffull || nblk > 0xfffffffeull) return LSMGPU_ERR_TOO_LARGE;
+  HIPC(hipSetDevice(c->device));
+  HIPC(hipMemsetAsync(d_result, 0, 8 * sizeof(uint64_t), c->stream));
+  if (nblk == 0) {
+    if (out->blk_first) HIPC(hipMemsetAsync(out->blk_first, 0, 4, c->stream));
+    return LSMGPU_OK;
+  }
+  if (!d_data || !d_blk_off || !d_blk_len) return LSMGPU_ERR_ARG;
+  size_t need = (size_t)nblk * 64;
+  if (need > c->lb.cap) {
+    HIPC(hipStreamSynchronize(c->stream));
+    HIPC(c->lb.ensure(need));
+    HIPC(hipMemset(c->lb.p, 0, c->lb.cap));
+  }
+  next_tag(c, nblk);
+  DecodeParams p{};
+  p.data = d_data;
+  p.data_len = data_len;
+  p.blk_off = d_blk_off;
+  p.blk_len = d_blk_len;
+  p.nblk = (uint32_t)nblk;
+  p.mode = mode;
+  p.key_data = out->key_data;
+  p.key_cap = out->key_cap;
+  p.key_end = out->key_end;
+  p.val_data = out->val_data;
+  p.val_cap = out->val_cap;
+  p.val_end = out->val_end;
+  p.view = out->view;
+  p.ent_cap = out->ent_cap;
+  p.blk_first = out->blk_first;
+  p.blk_status = out->blk_status;
+  p.lb = c->lb.as<uint64_t>();
+  p.ticket = c->ticket.as<unsigned long long>();
+  p.ticket_base = c->ticket_val;
+  p.result = d_result;
+  p.tag = c->tag;
+  uint64_t waves = 0;
+  HIPC(launch_decode(p, max_blk_len, c->num_cus, c->stream, &waves));
+  c->ticket_val += nblk + waves;  // every wave draws tickets until one is >= nblk
+  return LSMGPU_OK;
+}
+
+int lsmgpu_decode_blocks(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
+                         int data_on_device, const uint32_t* blk_off, const uint32_t* blk_len,
+                         uint64_t nblk, int mode, lsmgpu_decoded* out) {
+  if (!c || !out) return LSMGPU_ERR_ARG;
+  if (nblk && (!blk_off || !blk_len || !data)) return LSMGPU_ERR_ARG;
+  if (data_len > 0xffffffffull) return LSMGPU_ERR_TOO_LARGE;
+  HIPC(hipSetDevice(c->device));
+  uint32_t max_len = 0;
+  for (uint64_t b = 0; b < nblk; b++) max_len = std::max(max_len, blk_len[b]);
+  HIPC(c->s_off.ensure((nblk + 1) * 4));
+  HIPC(c->s_len.ensure((nblk + 1) * 4));
+  if (nblk) {
+    HIPC(hipMemcpyAsync(c->s_off.p, blk_off, nblk * 4, hipMemcpyHostToDevice, c->stream));
+    HIPC(hipMemcpyAsync(c->s_len.p, blk_len, nblk * 4, hipMemcpyHostToDevice, c->stream));
+  }
+  lsmgpu_decoded d = *out;
+  const uint8_t* d_data = data;
+  if (!data_on_device) {  // stage host buffers through HBM
+    HIPC(c->s_data.ensure(data_len + 16));
+    if (data_len) HIPC(hipMemcpyAsync(c->s_data.p, data, data_len, hipMemcpyHostToDevice, c->stream));
+    d_data = c->s_data.as<uint8_t>();
+    auto stage = [&](DevBuf& b, void* hp, uint64_t bytes) -> void* {
+      if (!hp) return nullptr;
+      if (b.ensure(bytes + 16) != hipSuccess) return (void*)-1;
+      return b.p;
+    };
+    d.key_data = (uint8_t*)stage(c->s_kd, out->key_data, out->key_cap);
+    d.val_data = (uint8_t*)stage(c->s_vd, out->val_data, out->val_cap);
+    d.key_end = (uint32_t*)stage(c->s_ke, out->key_end, out->ent_cap * 4);
+    d.val_end = (uint32_t*)stage(c->s_ve, out->val_end, out->ent_cap * 4);
+    d.view = (uint64_t*)stage(c->s_view, out->view, out->ent_cap * 8);
+    d.blk_first = (uint32_t*)stage(c->s_bf, out->blk_first, (nblk + 1) * 4);
+    d.blk_status = (int32_t*)stage(c->s_bs, out->blk_status, nblk * 4);
+    void* ptrs[] = {d.key_data, d.val_data, d.key_end, d.val_end, d.view, d.blk_first, d.blk_status};
+    for (void* q : ptrs)
+      if (q == (void*)-1) return LSMGPU_ERR_HIP;
+  }
+  int rc = lsmgpu_decode_blocks_async(c, d_data, data_len, c->s_off.as<uint32_t>(),
+                                      c->s_len.as<uint32_t>(), nblk, max_len, mode, &d,
+                                      c->result.as<uint64_t>());
+  if (rc != LSMGPU_OK) return rc;
+  HIPC(hipMemcpyAsync(c->h_result, c->result.p, 64, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  const uint64_t* r = c->h_result;
+  out->n_entries = r[0];
+  out->key_bytes = r[1];
+  out->val_bytes = r[2];
+  out->first_bad_block = r[3] ? (int64_t)(nblk - r[3]) : -1;
+  out->n_bad_blocks = r[4];
+  const uint64_t flags = r[5];
+  if (!data_on_device) {
+    auto back = [&](void* hp, const void* dp, uint64_t bytes) -> hipError_t {
+      if (!hp || !bytes) return hipSuccess;
+      return hipMemcpyAsync(hp, dp, bytes, hipMemcpyDeviceToHost, c->stream);
+    };
+    const bool fits = !(flags & 1);
+    uint64_t ne = fits ? out->n_entries : 0;
+    if (fits) {
+      HIPC(back(out->key_data, d.key_data, std::min(out->key_cap, out->key_bytes)));
+      HIPC(back(out->val_data, d.val_data, std::min(out->val_cap, out->val_bytes)));
+      HIPC(back(out->key_end, d.key_end, ne * 4));
+      HIPC(back(out->val_end, d.val_end, ne * 4));
+      HIPC(back(out->view, d.view, ne * 8));
+    }
+    HIPC(back(out->blk_first, d.blk_first, (nblk + 1) * 4));
+    HIPC(back(out->blk_status, d.blk_status, nblk * 4));
+    HIPC(hipStreamSynchronize(c->stream));
+  }
+  if (flags & 2) return LSMGPU_ERR_INTERNAL;
+  if (flags & 1) return LSMGPU_ERR_CAPACITY;
+  return LSMGPU_OK;
+}
+
+// ------------------------------------------------------------------ encode
+int lsmgpu_plan_blocks(const uint32_t* key_end, const uint32_t* vs_end, uint64_t n,
+                       uint32_t epb, uint32_t block_bytes, uint32_t* blk_first, uint64_t cap,
+                       uint64_t* nblocks) {
+  if (!nblocks || (n && (!key_end || !vs_end))) return LSMGPU_ERR_ARG;
+  if (epb == 0 && block_bytes == 0) return LSMGPU_ERR_ARG;
+  // Builder.Add (builder.go:125-137) cut rule, plus the opt-in byte target
+  uint64_t nb = 0, counter = 0, cur = 0;
+  auto emit = [&](uint64_t e) {
+    if (blk_first && nb < cap) blk_first[nb] = (uint32_t)e;
+    nb++;
+  };
+  emit(0);
+  uint32_t k0 = 0, v0 = 0;
+  for (uint64_t e = 0; e < n; e++) {
+    uint64_t sz = 10ull + (key_end[e] - k0) + (vs_end[e] - v0);
+    k0 = key_end[e];
+    v0 = vs_end[e];
+    bool cut = (epb > 0 && counter >= epb);
+    if (!cut && block_bytes > 0 && counter > 0) cut = (cur + sz + 13) > block_bytes;
+    if (cut) {
+      emit(e);
+      counter = 0;
+      cur = 0;
+    }
+    counter++;
+    cur += sz;
+  }
+  if (blk_first && nb < cap) blk_first[nb] = (uint32_t)n;  // end sentinel
+  *nblocks = nb;
+  return (nb + 1 <= cap || !blk_first) ? LSMGPU_OK : LSMGPU_ERR_CAPACITY;
+}
+
+int lsmgpu_encode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_keys, const uint32_t* d_key_end,
+                               const uint8_t* d_vs, const uint32_t* d_vs_end, uint64_t n,
+                               uint32_t epb, const uint32_t* d_blk_first, uint64_t nblocks,
+                               uint64_t key_total, uint64_t vs_total, uint8_t* d_out,
+                               uint64_t out_cap, uint32_t* d_flags) {
+  if (!c || !d_out || !d_flags) return LSMGPU_ERR_ARG;
+  if (n && (!d_keys || !d_key_end || !d_vs || !d_vs_end)) return LSMGPU_ERR_ARG;
+  if (!d_blk_first && epb == 0) return LSMGPU_ERR_ARG;
+  if (!d_blk_first) nblocks = n ? (n + epb - 1) / epb : 1;
+  if (nblocks == 0) return LSMGPU_ERR_ARG;
+  uint64_t data_len = 10 * n + key_total + vs_total + 13 * nblocks;
+  uint64_t total = data_len + 4 * nblocks + 4;
+  if (data_len > 0xffffffffull) return LSMGPU_ERR_TOO_LARGE;
+  if (total > out_cap) return LSMGPU_ERR_CAPACITY;
+  HIPC(hipSetDevice(c->device));
+  EncodeParams p{};
+  p.keys = d_keys;
+  p.key_end = d_key_end;
+  p.vs = d_vs;
+  p.vs_end = d_vs_end;
+  p.n = n;
+  p.epb = epb;
+  p.blk_first = d_blk_first;
+  p.nblocks = (uint32_t)nblocks;
+  p.key_total = key_total;
+  p.vs_total = vs_total;
+  p.out = d_out;
+  p.data_len = data_len;
+  p.flags = d_flags;
+  HIPC(launch_encode(p, c->num_cus, c->stream));
+  return LSMGPU_OK;
+}
+
+int lsmgpu_encode_blocks(lsmgpu_ctx* c, const uint8_t* keys, const uint32_t* key_end,
+                         const uint8_t* vs, const uint32_t* vs_end, uint64_t n, int on_device,
+                         uint32_t epb, uint32_t block_bytes, uint8_t* out, uint64_t out_cap,
+                         uint64_t* out_len, uint64_t* data_len, uint32_t* restarts,
+                         uint64_t restarts_cap, uint64_t* nrestarts) {
+  if (!c || !out || !out_len) return LSMGPU_ERR_ARG;
+  if (n && (!keys || !key_end || !vs || !vs_end)) return LSMGPU_ERR_ARG;
+  if (epb == 0 && block_bytes == 0) return LSMGPU_ERR_ARG;
+  HIPC(hipSetDevice(c->device));
+  // host copies of the offset columns (needed for totals and the byte-target plan)
+  std::vector<uint32_t> hk, hv;
+  const uint32_t* hke = key_end;
+  const uint32_t* hve = vs_end;
+  if (on_device && n) {
+    hk.resize(n);
+    hv.resize(n);
+    HIPC(hipMemcpyAsync(hk.data(), key_end, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipMemcpyAsync(hv.data(), vs_end, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    hke = hk.data();
+    hve = hv.data();
+  }
+  const uint64_t key_total = n ? hke[n - 1] : 0, vs_total = n ? hve[n - 1] : 0;
+  for (uint64_t e = 0; e < n; e++) {  // host-side validation (also flagged on device)
+    uint64_t kl = hke[e] - (e ? hke[e - 1] : 0), vl = hve[e] - (e ? hve[e - 1] : 0);
+    if (kl <= 8 || kl > 0xffff) return LSMGPU_ERR_KEY_LEN;
+    if (vl > 0xffff) return LSMGPU_ERR_VALUE_LEN;
+  }
+  uint64_t nb = 0;
+  std::vector<uint32_t> plan;
+  const bool explicit_plan = block_bytes > 0;
+  if (explicit_plan) {
+    int rc = lsmgpu_plan_blocks(hke, hve, n, epb, block_bytes, nullptr, 0, &nb);
+    if (rc != LSMGPU_OK) return rc;
+    plan.resize(nb + 1);
+    rc = lsmgpu_plan_blocks(hke, hve, n, epb, block_bytes, plan.data(), nb + 1, &nb);
+    if (rc != LSMGPU_OK) return rc;
+  } else {
+    nb = n ? (n + epb - 1) / epb : 1;
+  }
+  const uint64_t dl = 10 * n + key_total + vs_total + 13 * nb;
+  const uint64_t total = dl + 4 * nb + 4;
+  *out_len = total;
+  if (data_len) *data_len = dl;
+  if (nrestarts) *nrestarts = nb;
+  if (dl > 0xffffffffull) return LSMGPU_ERR_TOO_LARGE;
+  if (total > out_cap) return LSMGPU_ERR_CAPACITY;
+
+  const uint8_t* dk = keys;
+  const uint32_t* dke = key_end;
+  const uint8_t* dv = vs;
+  const uint32_t* dve = vs_end;
+  uint8_t* dout = out;
+  if (!on_device) {
+    HIPC(c->s_a.ensure(key_total + 16));
+    HIPC(c->s_b.ensure(n * 4 + 16));
+    HIPC(c->s_c.ensure(vs_total + 16));
+    HIPC(c->s_d.ensure(n * 4 + 16));
+    HIPC(c->s_kd.ensure(total + 16));
+    if (key_total) HIPC(hipMemcpyAsync(c->s_a.p, keys, key_total, hipMemcpyHostToDevice, c->stream));
+    if (vs_total) HIPC(hipMemcpyAsync(c->s_c.p, vs, vs_total, hipMemcpyHostToDevice, c->stream));
+    if (n) {
+      HIPC(hipMemcpyAsync(c->s_b.p, key_end, n * 4, hipMemcpyHostToDevice, c->stream));
+      HIPC(hipMemcpyAsync(c->s_d.p, vs_end, n * 4, hipMemcpyHostToDevice, c->stream));
+    }
+    dk = c->s_a.as<uint8_t>();
+    dke = c->s_b.as<uint32_t>();
+    dv = c->s_c.as<uint8_t>();
+    dve = c->s_d.as<uint32_t>();
+    dout = c->s_kd.as<uint8_t>();
+  }
+  const uint32_t* dplan = nullptr;
+  if (explicit_plan) {
+    HIPC(c->s_bf.ensure((nb + 1) * 4));
+    HIPC(hipMemcpyAsync(c->s_bf.p, plan.data(), (nb + 1) * 4, hipMemcpyHostToDevice, c->stream));
+    dplan = c->s_bf.as<uint32_t>();
+  }
+  HIPC(hipMemsetAsync(c->flags.p, 0, 16, c->stream));
+  int rc = lsmgpu_encode_blocks_async(c, dk, dke, dv, dve, n, epb, dplan, nb, key_total, vs_total,
+                                      dout, total, c->flags.as<uint32_t>());
+  if (rc != LSMGPU_OK) return rc;
+  uint32_t hflags[4] = {0, 0, 0, 0};
+  HIPC(hipMemcpyAsync(hflags, c->flags.p, 16, hipMemcpyDeviceToHost, c->stream));
+  if (!on_device) HIPC(hipMemcpyAsync(out, dout, total, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  if (hflags[0] & 1) return LSMGPU_ERR_KEY_LEN;
+  if (hflags[0] & 2) return LSMGPU_ERR_VALUE_LEN;
+  if (restarts) {
+    if (nb > restarts_cap) return LSMGPU_ERR_CAPACITY;
+    std::vector<uint8_t> idx(4 * nb);
+    if (on_device) {
+      HIPC(hipMemcpy(idx.data(), out + dl, 4 * nb, hipMemcpyDeviceToHost));
+    } else {
+      std::memcpy(idx.data(), out + dl, 4 * nb);
+    }
+    for (uint64_t b = 0; b < nb; b++) restarts[b] = rd_be32(idx.data() + 4 * b);
+  }
+  return LSMGPU_OK;
+}
+
+// ------------------------------------------------------------------ ValueStruct columns
+int lsmgpu_encode_values(lsmgpu_ctx* c, const uint8_t* meta, const uint8_t* user_meta,
+                         const uint64_t* expires_at, const uint8_t* values,
+                         const uint32_t* value_end, uint64_t n, int on_device, uint8_t* vs,
+                         uint64_t vs_cap, uint32_t* vs_end, uint64_t* vs_len) {
+  if (!c || !vs_len) return LSMGPU_ERR_ARG;
+  *vs_len = 0;
+  if (n == 0) return LSMGPU_OK;
+  if (!meta || !user_meta || !expires_at || !value_end || !vs || !vs_end) return LSMGPU_ERR_ARG;
+  HIPC(hipSetDevice(c->device));
+  uint64_t vtotal = 0;
+  if (on_device) {
+    uint32_t last = 0;
+    HIPC(hipMemcpyAsync(&last, value_end + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    vtotal = last;
+  } else {
+    vtotal = value_end[n - 1];
+  }
+  if (!values && vtotal) return LSMGPU_ERR_ARG;
+  ValuesParams p{};
+  p.n = n;
+  if (on_device) {
+    p.meta = meta; p.user_meta = user_meta; p.expires_at = expires_at; p.values = values;
+    p.value_end = value_end; p.vs = vs; p.vs_end = vs_end;
+  } else {
+    HIPC(c->s_a.ensure(n * 2 + 16));
+    HIPC(c->s_b.ensure(n * 8 + 16));
+    HIPC(c->s_c.ensure(vtotal + 16));
+    HIPC(c->s_d.ensure(n * 4 + 16));
+    HIPC(c->s_ve.ensure(n * 4 + 16));
+    uint8_t* dm = c->s_a.as<uint8_t>();
+    HIPC(hipMemcpyAsync(dm, meta, n, hipMemcpyHostToDevice, c->stream));
+    HIPC(hipMemcpyAsync(dm + n, user_meta, n, hipMemcpyHostToDevice, c->stream));
+    HIPC(hipMemcpyAsync(c->s_b.p, expires_at, n * 8, hipMemcpyHostToDevice, c->stream));
+    if (vtotal) HIPC(hipMemcpyAsync(c->s_c.p, values, vtotal, hipMemcpyHostToDevice, c->stream));
+    HIPC(hipMemcpyAsync(c->s_d.p, value_end, n * 4, hipMemcpyHostToDevice, c->stream));
+    p.meta = dm; p.user_meta = dm + n; p.expires_at = c->s_b.as<uint64_t>();
+    p.values = c->s_c.as<uint8_t>(); p.value_end = c->s_d.as<uint32_t>();
+    p.vs_end = c->s_ve.as<uint32_t>();
+  }
+  // sizes -> scratch, inclusive scan -> vs_end (rocPRIM device scan)
+  uint32_t* final_end = p.vs_end;
+  HIPC(c->s_view.ensure(n * 4 + 16));
+  p.vs_end = c->s_view.as<uint32_t>();
+  HIPC(launch_values_sizes(p, c->stream));
+  size_t tmp = 0;
+  HIPC(rocprim::inclusive_scan(nullptr, tmp, p.vs_end, final_end, (size_t)n,
+                               rocprim::plus<uint32_t>(), c->stream));
+  HIPC(c->scan_tmp.ensure(tmp + 16));
+  HIPC(rocprim::inclusive_scan(c->scan_tmp.p, tmp, p.vs_end, final_end, (size_t)n,
+                               rocprim::plus<uint32_t>(), c->stream));
+  p.vs_end = final_end;
+  uint32_t total = 0;
+  HIPC(hipMemcpyAsync(&total, p.vs_end + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  *vs_len = total;
+  if (total > vs_cap) return LSMGPU_ERR_CAPACITY;
+  if (!on_device) {
+    HIPC(c->s_kd.ensure((uint64_t)total + 16));
+    p.vs = c->s_kd.as<uint8_t>();
+  }
+  HIPC(launch_values_write(p, c->stream));
+  if (!on_device) {
+    HIPC(hipMemcpyAsync(vs, p.vs, total, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipMemcpyAsync(vs_end, p.vs_end, n * 4, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPC(hipStreamSynchronize(c->stream));
+  return LSMGPU_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,69 @@
+// kernels.hpp -- launch interface between the C ABI (api.hip) and the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lsmgpu {
+
+// Decode: one wave per SST data block, blocks taken in ticket order (decoupled look-back
+// over per-block {entries, key bytes, value bytes}).  See DESIGN.md "decode kernel".
+struct DecodeParams {
+  const uint8_t* data;
+  uint64_t data_len;
+  const uint32_t* blk_off;
+  const uint32_t* blk_len;
+  uint32_t nblk;
+  int mode;
+  uint8_t* key_data;
+  uint64_t key_cap;
+  uint32_t* key_end;
+  uint8_t* val_data;
+  uint64_t val_cap;
+  uint32_t* val_end;
+  uint64_t* view;
+  uint64_t ent_cap;
+  uint32_t* blk_first;
+  int32_t* blk_status;
+  uint64_t* lb;             // look-back granules, 8 u64 per block
+  unsigned long long* ticket;  // monotonic ticket counter (never reset)
+  uint64_t ticket_base;     // counter value at launch
+  uint64_t* result;         // 8 u64, zeroed before launch
+  uint32_t tag;             // 24-bit epoch tag of this launch
+};
+
+// Encode: one wave per output block; every byte position is closed-form
+// (pos(e) = 10e + key_start(e) + vs_start(e) + 13*block(e)), so no scan is needed.
+struct EncodeParams {
+  const uint8_t* keys;
+  const uint32_t* key_end;
+  const uint8_t* vs;
+  const uint32_t* vs_end;
+  uint64_t n;
+  uint32_t epb;               // entries per block (when blk_first == nullptr)
+  const uint32_t* blk_first;  // optional explicit plan (nblocks+1)
+  uint32_t nblocks;
+  uint64_t key_total, vs_total;
+  uint8_t* out;
+  uint64_t data_len;          // size of the data region (index starts here)
+  uint32_t* flags;
+};
+
+struct ValuesParams {
+  const uint8_t* meta;
+  const uint8_t* user_meta;
+  const uint64_t* expires_at;
+  const uint8_t* values;
+  const uint32_t* value_end;
+  uint64_t n;
+  uint8_t* vs;
+  uint32_t* vs_end;   // input: already holds the scanned end offsets
+};
+
+// launchers (return hipError_t)
+hipError_t launch_decode(const DecodeParams& p, uint32_t max_blk_len, int num_cus,
+                         hipStream_t s, uint64_t* waves_launched);
+hipError_t launch_encode(const EncodeParams& p, int num_cus, hipStream_t s);
+hipError_t launch_values_sizes(const ValuesParams& p, hipStream_t s);
+hipError_t launch_values_write(const ValuesParams& p, hipStream_t s);
+
+}  // namespace lsmgpu

@@ -1,0 +1,245 @@
+"""GPU parity: the gfx950 decode/encode kernels (through the C ABI) vs the CPU oracle.
+
+Bit-exact for every output (integer/byte work).  Inputs: hand-derived KATs, the committed
+golden fixtures, and seeded synthetic tables of every BASELINE config at oracle-sized scales.
+"""
+import numpy as np
+import pytest
+
+import kat_defs as K
+from lsmdb_amd import workload
+
+pytestmark = pytest.mark.gpu
+
+
+def _assert_same(g, o, label=""):
+    assert g.n_entries == o.n_entries, label
+    assert np.array_equal(g.blk_status, o.blk_status), label
+    assert np.array_equal(g.blk_first, o.blk_first), label
+    assert np.array_equal(g.key_end, o.key_end), label
+    assert np.array_equal(g.val_end, o.val_end), label
+    assert g.key_data.tobytes() == o.key_data.tobytes(), label
+    assert g.val_data.tobytes() == o.val_data.tobytes(), label
+    if g.view is not None:
+        assert np.array_equal(g.view, o.view), label
+    assert g.first_bad_block == o.first_bad_block, label
+    assert g.n_bad_blocks == o.n_bad_blocks, label
+
+
+@pytest.mark.parametrize("name,block,entries,status", K.DECODE_KATS)
+def test_decode_kat_gpu(codec, name, block, entries, status):
+    pad = b"\xee" * 7
+    data = pad + block + pad
+    g = codec.decode_host(data, np.array([len(pad)], np.uint32), np.array([len(block)], np.uint32))
+    assert int(g.blk_status[0]) == status, name
+    assert g.n_entries == len(entries)
+    for i, (k, v) in enumerate(entries):
+        assert g.key(i) == k
+        assert g.value(i) == v
+
+
+def test_decode_kats_batched(codec, oracle):
+    """All KAT blocks in ONE batch, each at a different alignment (look-back across error
+    blocks, mixed statuses, zero-length blocks)."""
+    data = bytearray()
+    offs, lens = [], []
+    for i, (_n, block, _e, _s) in enumerate(K.DECODE_KATS * 3):
+        data += b"\xab" * (i % 13)
+        offs.append(len(data))
+        lens.append(len(block))
+        data += block
+    data = bytes(data)
+    off, ln = np.array(offs, np.uint32), np.array(lens, np.uint32)
+    _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln))
+
+
+@pytest.mark.parametrize("name,keys,vss,epb,data,index", K.BUILDER_KATS)
+def test_encode_kat_gpu(codec, oracle, name, keys, vss, epb, data, index):
+    kb, ke, vb, ve = oracle.columns(keys, vss)
+    out, data_len, restarts = codec.encode_host(kb, ke, vb, ve, entries_per_block=epb)
+    assert data_len == len(data)
+    assert out == data + index, name
+
+
+def _cols(cfg, n, seed=0):
+    c = workload.config_columns(cfg, n, seed)
+    return c
+
+
+@pytest.mark.parametrize("cfg,n", [(1, 10000), (2, 20000), (3, 3000), (4, 12000), (5, 20000),
+                                   (1, 101), (1, 199), (1, 200), (1, 250), (2, 1), (5, 7)])
+def test_encode_decode_vs_oracle(codec, oracle, cfg, n):
+    c = _cols(cfg, n, seed=n)
+    ref, ref_dl, ref_rs = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end,
+                                            c.entries_per_block, c.block_bytes)
+    out, dl, rs = codec.encode_host(c.keys, c.key_end, c.vs, c.vs_end, c.entries_per_block,
+                                    c.block_bytes)
+    assert dl == ref_dl
+    assert np.array_equal(rs, ref_rs)
+    assert out == ref, f"encode mismatch cfg={cfg} n={n}"
+    # decode the oracle's bytes on the GPU, compare with the oracle decode
+    tail = b"{}" + (2).to_bytes(4, "big")
+    sst = ref + tail
+    off, ln, _, _ = oracle.parse_index(sst)
+    g = codec.decode_host(sst, off, ln)
+    o = oracle.decode(sst, off, ln)
+    _assert_same(g, o, f"cfg={cfg}")
+    # round trip: decoded streams are the encoder's inputs
+    assert g.key_data.tobytes() == c.keys.tobytes()
+    assert g.val_data.tobytes() == c.vs.tobytes()
+    assert np.array_equal(g.key_end, c.key_end)
+    assert np.array_equal(g.val_end, c.vs_end)
+
+
+def _sst_blocks(oracle, parts):
+    data = b"".join(parts)
+    offs, lens, base = [], [], 0
+    for p in parts:
+        o, l, _, _ = oracle.parse_index(p + b"{}" + (2).to_bytes(4, "big"))
+        offs.append(o + base)
+        lens.append(l)
+        base += len(p)
+    return data, np.concatenate(offs).astype(np.uint32), np.concatenate(lens).astype(np.uint32)
+
+
+def test_slow_paths(codec, oracle):
+    """Blocks larger than every LDS slot (global path), blocks with more entries than the
+    slot's metadata capacity, and both mixed with ordinary blocks in one batch."""
+    big = _cols(3, 300, seed=1)  # 1 KiB values, 100 entries/block -> ~110 KiB blocks
+    sst_big, _, _ = oracle.build_cols(big.keys, big.key_end, big.vs, big.vs_end, 100, 0)
+    keys = [b"k%08d" % i for i in range(2000)]           # 9-B keys, 3-B values: 22-B entries
+    vss = [b"\x41\x00\x00" for _ in range(2000)]
+    sst_many, _, _ = oracle.build(keys, vss, entries_per_block=180)  # 180 entries in < 4 KiB
+    small = _cols(2, 500, seed=2)
+    sst_small, _, _ = oracle.build_cols(small.keys, small.key_end, small.vs, small.vs_end, 0, 4096)
+    for parts in ([sst_big], [sst_many], [sst_small, sst_many], [sst_big, sst_many, sst_small]):
+        data, off, ln = _sst_blocks(oracle, parts)
+        _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln))
+    # encode of oversize / many-entry blocks (slow encode paths) stays bit-exact
+    out, _, _ = codec.encode_host(big.keys, big.key_end, big.vs, big.vs_end, 100, 0)
+    assert out == sst_big
+    kb, ke, vb, ve = oracle.columns(keys, vss)
+    out2, _, _ = codec.encode_host(kb, ke, vb, ve, 180, 0)
+    assert out2 == sst_many
+    out3, _, _ = codec.encode_host(kb, ke, vb, ve, 2000, 0)
+    ref3, _, _ = oracle.build(keys, vss, entries_per_block=2000)
+    assert out3 == ref3
+
+
+def test_prefix_compressed_random(codec, oracle):
+    """Random hand-built prefix-compressed blocks (plen > 0): the decoder's general rule."""
+    import struct
+    rng = np.random.default_rng(7)
+    data = bytearray()
+    offs, lens = [], []
+    for b in range(300):
+        blk = bytearray()
+        n = int(rng.integers(1, 40))
+        base = bytes(rng.integers(0, 256, int(rng.integers(9, 40)), dtype=np.uint8))
+        prev = 0xFFFFFFFF
+        for e in range(n):
+            pos = len(blk)
+            if e == 0:
+                plen, diff = 0, base
+            else:
+                plen = int(rng.integers(0, len(base) + 5))
+                diff = bytes(rng.integers(0, 256, int(rng.integers(0, 20)), dtype=np.uint8))
+                if plen == 0 and not diff:
+                    diff = b"x"
+            val = bytes(rng.integers(0, 256, int(rng.integers(0, 60)), dtype=np.uint8))
+            blk += struct.pack(">HHHI", plen, len(diff), len(val), prev) + diff + val
+            prev = pos
+        blk += struct.pack(">HHHI", 0, 0, 3, prev) + b"\0\0\0"
+        data += b"\x00" * int(rng.integers(0, 9))
+        offs.append(len(data))
+        lens.append(len(blk))
+        data += blk
+    data = bytes(data)
+    off, ln = np.array(offs, np.uint32), np.array(lens, np.uint32)
+    _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln))
+
+
+def test_device_resident_async(codec, oracle):
+    """The benchmarked entry point (all pointers on device) on a C2 table."""
+    import torch
+    c = _cols(2, 40000, seed=3)
+    ref, ref_dl, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, 0, 4096)
+    sst = ref + b"{}" + (2).to_bytes(4, "big")
+    off, ln, _, _ = oracle.parse_index(sst)
+    dev = torch.device("cuda", 0)
+    d_data = torch.from_numpy(np.frombuffer(sst, np.uint8).copy()).to(dev)
+    d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+    d_len = torch.from_numpy(ln.view(np.int32)).to(dev)
+    for mode in (1, 2, 3):
+        bufs = codec.alloc_decode(len(sst), int(ln.sum()), off.size, mode)
+        for _rep in range(3):  # repeated launches: epoch tags / ticket bases
+            codec.decode_device_async(d_data, d_off, d_len, int(ln.max()), mode, bufs)
+        codec.synchronize()
+        res = bufs.result.cpu().numpy()
+        o = oracle.decode(sst, off, ln)
+        assert res[0] == o.n_entries
+        assert res[1] == len(o.key_data) and res[2] == len(o.val_data)
+        assert res[5] == 0
+        n = o.n_entries
+        assert np.array_equal(bufs.blk_first.cpu().numpy().view(np.uint32), o.blk_first)
+        if mode & 1:
+            assert bufs.key_data[: int(res[1])].cpu().numpy().tobytes() == o.key_data.tobytes()
+            assert bufs.val_data[: int(res[2])].cpu().numpy().tobytes() == o.val_data.tobytes()
+            assert np.array_equal(bufs.key_end[:n].cpu().numpy().view(np.uint32), o.key_end)
+            assert np.array_equal(bufs.val_end[:n].cpu().numpy().view(np.uint32), o.val_end)
+        if mode & 2:
+            assert np.array_equal(bufs.view[:n].cpu().numpy().view(np.uint64), o.view)
+
+
+def test_capacity_overflow_reported(codec, oracle):
+    c = _cols(1, 1000, seed=4)
+    ref, _, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, 100, 0)
+    sst = ref + b"{}" + (2).to_bytes(4, "big")
+    off, ln, _, _ = oracle.parse_index(sst)
+    import torch
+    dev = torch.device("cuda", 0)
+    d_data = torch.from_numpy(np.frombuffer(sst, np.uint8).copy()).to(dev)
+    d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+    d_len = torch.from_numpy(ln.view(np.int32)).to(dev)
+    bufs = codec.alloc_decode(len(sst), 1000, off.size, 1)  # far too small
+    codec.decode_device_async(d_data, d_off, d_len, int(ln.max()), 1, bufs)
+    codec.synchronize()
+    res = bufs.result.cpu().numpy()
+    assert res[5] & 1  # capacity flag; totals still exact
+    o = oracle.decode(sst, off, ln)
+    assert res[0] == o.n_entries
+
+
+def test_encode_values_gpu(codec, oracle):
+    rng = np.random.default_rng(11)
+    n = 5000
+    meta = rng.integers(0, 256, n, dtype=np.uint8)
+    um = rng.integers(0, 256, n, dtype=np.uint8)
+    r = rng.integers(0, np.iinfo(np.uint64).max, n, dtype=np.uint64, endpoint=True)
+    exp = r >> rng.integers(0, 64, n).astype(np.uint64)
+    exp[rng.random(n) < 0.3] = 0
+    lens = rng.integers(0, 200, n)
+    vals = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    vend = np.cumsum(lens).astype(np.uint32)
+    vs, vs_end = codec.encode_values_host(meta, um, exp, vals.tobytes(), vend)
+    exp_bytes = b""
+    parts = []
+    s = 0
+    for i in range(n):
+        e = int(vend[i])
+        parts.append(oracle.vs_encode(int(meta[i]), int(um[i]), int(exp[i]), vals[s:e].tobytes()))
+        s = e
+    exp_bytes = b"".join(parts)
+    assert vs == exp_bytes
+    assert np.array_equal(vs_end, np.cumsum([len(p) for p in parts]).astype(np.uint32))
+
+
+def test_encode_rejects_bad_keys(codec):
+    from lsmdb_amd._lib import LsmgpuError
+    keys = [b"short"]
+    kb = b"".join(keys)
+    ke = np.array([5], np.uint32)
+    vb = b"\x41\x00\x00"
+    ve = np.array([3], np.uint32)
+    with pytest.raises(LsmgpuError):
+        codec.encode_host(kb, ke, vb, ve, 100, 0)
