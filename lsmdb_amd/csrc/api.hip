@@ -17,7 +17,7 @@ using namespace lsmgpu;
 
 namespace {
 
-constexpr uint32_t kTagMax = (1u << 24) - 1;
+constexpr uint32_t kTagMax = 0xfffffffeu;
 
 struct DevBuf {
   void* p = nullptr;
@@ -52,8 +52,6 @@ struct lsmgpu_ctx {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   DevBuf lb;             // look-back granules (64 B per block)
-  DevBuf ticket;         // u64 monotonic ticket counter
-  uint64_t ticket_val = 0;
   DevBuf result;         // 8 x u64
   uint64_t* h_result = nullptr;  // pinned
   uint32_t tag = 0;
@@ -106,14 +104,11 @@ int lsmgpu_open(int device, lsmgpu_ctx** out) {
     return LSMGPU_ERR_HIP;
   }
   c->stream = c->own_stream;
-  if (c->ticket.ensure(64) != hipSuccess || c->result.ensure(64) != hipSuccess ||
-      c->flags.ensure(64) != hipSuccess ||
-      hipHostMalloc(reinterpret_cast<void**>(&c->h_result), 64, hipHostMallocDefault) != hipSuccess ||
-      hipMemset(c->ticket.p, 0, 64) != hipSuccess) {
+  if (c->result.ensure(64) != hipSuccess || c->flags.ensure(64) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&c->h_result), 64, hipHostMallocDefault) != hipSuccess) {
     lsmgpu_close(c);
     return LSMGPU_ERR_HIP;
   }
-  c->ticket_val = 0;
   *out = c;
   return LSMGPU_OK;
 }
@@ -122,7 +117,7 @@ void lsmgpu_close(lsmgpu_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
-  DevBuf* bufs[] = {&c->lb, &c->ticket, &c->result, &c->flags, &c->scan_tmp, &c->s_data,
+  DevBuf* bufs[] = {&c->lb, &c->result, &c->flags, &c->scan_tmp, &c->s_data,
                     &c->s_off, &c->s_len, &c->s_kd, &c->s_ke, &c->s_vd, &c->s_ve, &c->s_view,
                     &c->s_bf, &c->s_bs, &c->s_a, &c->s_b, &c->s_c, &c->s_d};
   for (DevBuf* b : bufs) b->release();
@@ -198,13 +193,17 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     return LSMGPU_OK;
   }
   if (!d_data || !d_blk_off || !d_blk_len) return LSMGPU_ERR_ARG;
-  size_t need = (size_t)nblk * 64;
+  // layout: [gcnt: ngroups u32, padded to 256 B][block records 64 B x nblk][group records 64 B]
+  const uint64_t ngroups = (nblk + 63) / 64;
+  const size_t cnt_bytes = (size_t)((ngroups * 4 + 255) / 256 * 256);
+  size_t need = cnt_bytes + (size_t)nblk * 64 + (size_t)ngroups * 64;
   if (need > c->lb.cap) {
     HIPC(hipStreamSynchronize(c->stream));
     HIPC(c->lb.ensure(need));
     HIPC(hipMemset(c->lb.p, 0, c->lb.cap));
   }
   next_tag(c, nblk);
+  HIPC(hipMemsetAsync(c->lb.p, 0, cnt_bytes, c->stream));
   DecodeParams p{};
   p.data = d_data;
   p.data_len = data_len;
@@ -222,14 +221,14 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
   p.ent_cap = out->ent_cap;
   p.blk_first = out->blk_first;
   p.blk_status = out->blk_status;
-  p.lb = c->lb.as<uint64_t>();
-  p.ticket = c->ticket.as<unsigned long long>();
-  p.ticket_base = c->ticket_val;
+  p.gcnt = c->lb.as<uint32_t>();
+  p.lb = reinterpret_cast<uint64_t*>(c->lb.as<uint8_t>() + cnt_bytes);
+  p.glb = p.lb + nblk * 8;
   p.result = d_result;
   p.tag = c->tag;
   uint64_t waves = 0;
   HIPC(launch_decode(p, max_blk_len, c->num_cus, c->stream, &waves));
-  c->ticket_val += nblk + waves;  // every wave draws tickets until one is >= nblk
+  (void)waves;
   return LSMGPU_OK;
 }
 

@@ -35,10 +35,16 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 }
 
 // ---------------------------------------------------------------- agent-scope granules
-// Look-back state: 8-byte {tag:24 | value:40} granules written by ONE atomic (sc1) store
-// and read by relaxed agent-scope loads (MI355X_MICROARCH: R2 granule hand-off).
-constexpr int kTagShift = 40;
-constexpr uint64_t kValMask = (1ull << kTagShift) - 1;
+// Prefix state: 8-byte {tag:32 | value:32} granules written by ONE atomic (sc1) store and
+// read by relaxed agent-scope loads (MI355X_MICROARCH: R2 granule hand-off).  Values are
+// u32 with saturating adds (a key stream past 4 GiB - 1 saturates and fails the capacity
+// check; entries and value bytes are bounded by the <= 4 GiB - 1 input).
+constexpr int kTagShift = 32;
+constexpr uint64_t kValMask = 0xffffffffull;
+__device__ __forceinline__ uint32_t sat_add(uint32_t a, uint32_t b) {
+  const uint32_t s = a + b;
+  return s < a ? 0xffffffffu : s;
+}
 __device__ __forceinline__ uint64_t gload(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

@@ -5,8 +5,8 @@
 
 namespace lsmgpu {
 
-// Decode: one wave per SST data block, blocks taken in ticket order (decoupled look-back
-// over per-block {entries, key bytes, value bytes}).  See DESIGN.md "decode kernel".
+// Decode: one wave per SST data block over a persistent, fully resident grid; output bases
+// from a two-level prefix over per-block {entries, key bytes, value bytes}.  DESIGN.md.
 struct DecodeParams {
   const uint8_t* data;
   uint64_t data_len;
@@ -24,11 +24,12 @@ struct DecodeParams {
   uint64_t ent_cap;
   uint32_t* blk_first;
   int32_t* blk_status;
-  uint64_t* lb;             // look-back granules, 8 u64 per block
-  unsigned long long* ticket;  // monotonic ticket counter (never reset)
-  uint64_t ticket_base;     // counter value at launch
+  uint64_t* lb;             // per-block records: aggregate [0..2], exclusive prefix [4..6]
+  uint64_t* glb;            // per-group records (64 blocks): aggregate [0..2], inclusive [4..6]
+  uint32_t* gcnt;           // per-group arrival counters, zeroed before launch
   uint64_t* result;         // 8 u64, zeroed before launch
   uint32_t tag;             // 24-bit epoch tag of this launch
+  uint32_t ablate;          // timing-only diagnostics (LSMGPU_ABLATE): 1 no prefix, 2 no emit, 4 no walk
 };
 
 // Encode: one wave per output block; every byte position is closed-form
