@@ -109,66 +109,66 @@ __device__ __forceinline__ uint32_t wave_scan_incl32(uint32_t v, uint32_t lane) 
 // whose size differs from the stride, and every lane before it is a confirmed entry.  A
 // round therefore advances over a whole run of equal-size entries with ONE LDS round trip;
 // a size change simply starts the next round at the mismatching entry's successor.
-constexpr uint32_t kEntry = 0, kEnd = 1, kTrunc = 2, kTerm = 3, kFirstPlen = 4, kPrefixOob = 5,
-                   kValOvf = 6, kOff = 7;
 struct SpecResult {
   uint32_t n, status, base_pos, end_pos;
 };
+__device__ __forceinline__ uint32_t readlane(uint32_t v, uint32_t l) {
+  return __builtin_amdgcn_readlane(v, l);
+}
+// Status of the iterator at a position where no entry was confirmed (walk_block's rules).
+__device__ __forceinline__ SpecResult stop_at(const LdsSrc& src, uint32_t pf, uint32_t len,
+                                              uint32_t n, uint32_t base_pos, bool first) {
+  uint32_t st = LSMGPU_BLK_OK, end = pf;
+  if (pf < len) {                                          // else: pos >= len, io.EOF
+    if (len - pf < 10) {
+      st = LSMGPU_BLK_TRUNC_HEADER;
+    } else {
+      const Hdr h = src.hdr(pf);
+      if ((h.klen | h.plen) == 0) end = pf + 10;            // terminator
+      else if (first && h.plen != 0) st = LSMGPU_BLK_FIRST_PLEN;
+      else if (base_pos + h.plen > len) st = LSMGPU_BLK_PREFIX_OOB;
+      else st = LSMGPU_BLK_VALUE_OVERFLOW;                  // p + 10 + klen + vlen > len
+    }
+  }
+  return SpecResult{n, st, base_pos, end};
+}
+
 __device__ __forceinline__ SpecResult walk_spec(const uint8_t* slot, uint32_t sh, uint32_t len,
                                                 uint16_t* meta, uint32_t maxe, uint32_t lane) {
   const LdsSrc src{slot, sh};
-  uint32_t pos = 0, n = 0, base_pos = 0, stride = 0;
-  bool have_base = false;
+  // first entry (uniform): defines baseKey (iterator.go:129-133) and the first stride guess
+  if (len < 10) return stop_at(src, 0, len, 0, 10, true);
+  const Hdr h0 = src.hdr(0);
+  const uint32_t base_pos = 10;
+  const uint32_t sz0 = 10 + h0.klen + h0.vlen;
+  if ((h0.klen | h0.plen) == 0 || h0.plen != 0 || base_pos + h0.plen > len || sz0 > len)
+    return stop_at(src, 0, len, 0, base_pos, true);
+  if (lane == 0 && maxe > 0) meta[0] = 0;
+  uint32_t pos = sz0, stride = sz0, n = 1;
   for (;;) {
+    // lane i checks the entry guessed at pos + i*stride (branch-free)
     const uint32_t p = pos + lane * stride;
-    const uint32_t bp = have_base ? base_pos : pos + 10;
-    uint32_t kind;
-    uint32_t sz = 0;
-    if (stride == 0 && lane != 0) {
-      kind = kOff;
-    } else if (p >= len) {
-      kind = kEnd;                                                    // iterator.go:115-118
-    } else if (len - p < 10) {
-      kind = kTrunc;
-    } else {
-      const Hdr h = src.hdr(p);
-      sz = 10 + h.klen + h.vlen;
-      if ((h.klen | h.plen) == 0) kind = kTerm;                       // iterator.go:124-127
-      else if (!have_base && lane == 0 && h.plen != 0) kind = kFirstPlen;  // iterator.go:131
-      else if (bp + h.plen > len) kind = kPrefixOob;
-      else if (p + sz > len) kind = kValOvf;                          // iterator.go:103-106
-      else kind = kEntry;
-    }
-    const bool entry = kind == kEntry;
-    const bool brk = entry && sz != stride;
-    const uint64_t any = __ballot(!entry || brk);
-    const uint32_t f = any ? (uint32_t)__builtin_ctzll(any) : 64u;
-    const bool f_brk = f < 64 && ((__ballot(brk) >> f) & 1ull);
-    const uint32_t m = f + (f_brk ? 1u : 0u);  // confirmed entries: lanes [0, m)
-    if (lane < m && n + lane < maxe) meta[4 * (n + lane)] = (uint16_t)p;  // header position
-    if (!have_base && m > 0) {
-      base_pos = pos + 10;
-      have_base = true;
-    }
-    n += m;
-    if (f == 64) {  // 64 entries of exactly `stride` bytes
+    const bool has_hdr = p + 10 <= len;
+    const Hdr h = src.hdr(has_hdr ? p : 0u);
+    const uint32_t sz = 10 + h.klen + h.vlen;
+    const bool bad = !has_hdr || (h.klen | h.plen) == 0 || base_pos + h.plen > len || p + sz > len;
+    const uint64_t any = __ballot(bad || sz != stride);
+    if (any == 0) {  // 64 entries of exactly `stride` bytes
+      if (n + lane < maxe) meta[4 * (n + lane)] = (uint16_t)p;
+      n += 64;
       pos += 64 * stride;
       continue;
     }
-    const uint32_t pf = __shfl(p, f);
-    if (f_brk) {  // entry f confirmed with another size: continue after it
-      const uint32_t szf = __shfl(sz, f);
-      pos = pf + szf;
-      if (f == 0) stride = szf;  // the guess failed at once: adopt the new size
-      continue;
-    }
-    const uint32_t kf = __shfl(kind, f);
-    uint32_t st = LSMGPU_BLK_OK;
-    if (kf == kTrunc) st = LSMGPU_BLK_TRUNC_HEADER;
-    else if (kf == kFirstPlen) st = LSMGPU_BLK_FIRST_PLEN;
-    else if (kf == kPrefixOob) st = LSMGPU_BLK_PREFIX_OOB;
-    else if (kf == kValOvf) st = LSMGPU_BLK_VALUE_OVERFLOW;
-    return SpecResult{n, st, base_pos, kf == kTerm ? pf + 10 : pf};
+    const uint32_t f = (uint32_t)__builtin_ctzll(any);
+    const bool fbad = (__ballot(bad) >> f) & 1ull;
+    const uint32_t m = f + (fbad ? 0u : 1u);  // confirmed entries: lanes [0, m)
+    if (lane < m && n + lane < maxe) meta[4 * (n + lane)] = (uint16_t)p;
+    n += m;
+    const uint32_t pf = readlane(p, f);
+    if (fbad) return stop_at(src, pf, len, n, base_pos, false);
+    const uint32_t szf = readlane(sz, f);  // entry f has another size: continue after it
+    pos = pf + szf;
+    if (f == 0) stride = szf;  // the guess failed at once: adopt the new size
   }
 }
 
@@ -176,9 +176,10 @@ __device__ __forceinline__ SpecResult walk_spec(const uint8_t* slot, uint32_t sh
 // the key / value output sizes) and row n into the totals sentinel.  Requires n <= maxe.
 __device__ __forceinline__ WalkResult finish_meta(const uint8_t* slot, uint32_t sh,
                                                   const SpecResult& r, uint16_t* meta,
-                                                  uint32_t lane) {
+                                                  uint32_t lane, bool& any_plen) {
   const LdsSrc src{slot, sh};
   uint32_t K = 0, V = 0;
+  any_plen = false;
   for (uint32_t e0 = 0; e0 < r.n; e0 += kWave) {
     const uint32_t e = e0 + lane;
     const bool on = e < r.n;
@@ -189,6 +190,7 @@ __device__ __forceinline__ WalkResult finish_meta(const uint8_t* slot, uint32_t 
       h = src.hdr(hp);
     }
     const uint32_t kl = on ? h.plen + h.klen : 0u, vl = on ? h.vlen : 0u;
+    any_plen = any_plen || __any(on && h.plen != 0);
     const uint32_t ki = wave_scan_incl32(kl, lane), vi = wave_scan_incl32(vl, lane);
     if (on)
       *reinterpret_cast<ushort4*>(meta + 4 * e) =
@@ -364,68 +366,153 @@ __device__ __forceinline__ void blend16(uint4& acc, const uint4& w, uint32_t a, 
   m = byte_mask(a, b, 3); acc.w = (acc.w & ~m) | (w.w & m);
 }
 
-// Writes stream bytes [0, L) of one block to dst (global, any alignment) as aligned 16-B
-// chunks gathered from the LDS copy of the block.  Stream byte t belongs to the entry e with
-// o(e) <= t < o(e+1), o = ko (keys) or vo (values) of the walk metadata (row n = totals).
-// Key bytes: u = t - ko(e) < plen(e) -> baseKey prefix (block byte base_pos + u), else the
-// stored diff (ks(e) + u - plen(e)) -- blockIterator.parseKV, iterator.go:98-100.  A chunk
-// is assembled from at most a few contiguous runs, each read as one unaligned 16-B window.
+// Stream bytes [t, hi) of one block assembled into a 16-B register image whose byte i is
+// stream byte t0 + i, starting from entry e (o(e) <= t).  Stream byte t of entry e: values
+// -> block byte vs(e) + (t - vo(e)); keys -> u = t - ko(e) < plen(e) ? baseKey prefix
+// (block byte base_pos + u) : stored diff (ks(e) + u - plen(e)) -- blockIterator.parseKV,
+// iterator.go:98-100.  Each contiguous run is one unaligned 16-B LDS window + a byte blend.
 template <bool IS_KEY>
-__device__ void gather_stream(uint8_t* dst, uint32_t L, const uint8_t* slot, uint32_t sh,
-                              const uint16_t* meta, uint32_t n, uint32_t base_pos,
-                              uint32_t lane) {
+__device__ __forceinline__ uint4 assemble(const uint8_t* slot, uint32_t sh, const uint16_t* meta,
+                                          uint32_t e, uint32_t base_pos, int32_t t0, uint32_t t,
+                                          uint32_t hi) {
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  ushort4 me = *reinterpret_cast<const ushort4*>(meta + 4 * e);
+  ushort4 mn = *reinterpret_cast<const ushort4*>(meta + 4 * e + 4);
+  while (t < hi) {
+    uint32_t o0 = IS_KEY ? me.y : me.w, o1 = IS_KEY ? mn.y : mn.w;
+    while (o1 <= t) {  // next entry (skips empty ones); never passes the sentinel since t < L
+      e++;
+      me = mn;
+      mn = *reinterpret_cast<const ushort4*>(meta + 4 * e + 4);
+      o0 = o1;
+      o1 = IS_KEY ? mn.y : mn.w;
+    }
+    const uint32_t u = t - o0;
+    uint32_t src, rend;
+    if (!IS_KEY) {
+      src = me.z + u;
+      rend = o1;
+    } else {
+      const uint32_t plen = (o1 - o0) - ((uint32_t)me.z - me.x);
+      if (u < plen) {
+        src = base_pos + u;
+        rend = o0 + plen;
+      } else {
+        src = me.x + (u - plen);
+        rend = o1;
+      }
+    }
+    if (rend > hi) rend = hi;
+    const uint32_t a = t - (uint32_t)t0;  // chunk byte of this run's start (0..15)
+    // window whose byte a is block byte src (>= 16 addressable LDS bytes precede the block)
+    const uint4 w = lds_u128(slot - 16, sh + src + 16 - a);
+    blend16(acc, w, a, rend - (uint32_t)t0);
+    t = rend;
+  }
+  return acc;
+}
+
+__device__ __forceinline__ void store_bytes(uint8_t* dst, const uint4& v, uint32_t a, uint32_t b) {
+  const uint32_t words[4] = {v.x, v.y, v.z, v.w};
+  for (uint32_t i = a; i < b; i++) dst[i] = (uint8_t)(words[i >> 2] >> (8 * (i & 3)));
+}
+
+// Writes stream bytes [0, L) of one block to dst (global, any alignment): lane e owns every
+// aligned 16-B output chunk whose first byte lies inside entry e's output range -- interior
+// chunks are one LDS window and one dwordx4 store; a chunk that crosses into later entries is
+// assembled run by run.  Entry 0's lane also writes the stream's leading partial chunk, and
+// the chunk past the stream end is written byte-wise (the neighbouring block owns the rest).
+template <bool IS_KEY>
+__device__ void emit_stream(uint8_t* dst, uint32_t L, const uint8_t* slot, uint32_t sh,
+                            const uint16_t* meta, uint32_t n, uint32_t base_pos, uint32_t lane) {
   if (L == 0) return;
   const uint32_t h = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);
-  uint8_t* dal = dst - h;
-  const uint32_t nchunk = (h + L + 15) >> 4;
-  const uint16_t* ocol = meta + (IS_KEY ? 1 : 3);
-  for (uint32_t c = lane; c < nchunk; c += kWave) {
-    const int32_t t0 = (int32_t)(c * 16) - (int32_t)h;
-    const uint32_t lo = t0 < 0 ? 0u : (uint32_t)t0;
-    const uint32_t hi = ((int32_t)L - t0 < 16) ? L : (uint32_t)(t0 + 16);
-    uint32_t e = meta_search(ocol, n, lo);
-    ushort4 me = *reinterpret_cast<const ushort4*>(meta + 4 * e);
-    ushort4 mn = *reinterpret_cast<const ushort4*>(meta + 4 * e + 4);
-    uint4 acc = make_uint4(0, 0, 0, 0);
-    uint32_t t = lo;
-    while (t < hi) {
-      uint32_t o0 = IS_KEY ? me.y : me.w, o1 = IS_KEY ? mn.y : mn.w;
-      while (o1 <= t) {  // next entry (skips empty ones); never passes row n since t < L
-        e++;
-        me = mn;
-        mn = *reinterpret_cast<const ushort4*>(meta + 4 * e + 4);
-        o0 = o1;
-        o1 = IS_KEY ? mn.y : mn.w;
+  uint8_t* dal = dst - h;  // chunk q covers stream bytes [16q - h, 16q - h + 16)
+  for (uint32_t e = lane; e < n; e += kWave) {
+    const ushort4 me = *reinterpret_cast<const ushort4*>(meta + 4 * e);
+    const ushort4 mn = *reinterpret_cast<const ushort4*>(meta + 4 * e + 4);
+    const uint32_t o0 = IS_KEY ? me.y : me.w, o1 = IS_KEY ? mn.y : mn.w;
+    if (e == 0 && h != 0) {  // leading partial chunk: stream bytes [0, min(16 - h, L))
+      const uint32_t hi = (16 - h < L) ? 16 - h : L;
+      const uint4 v = assemble<IS_KEY>(slot, sh, meta, 0, base_pos, -(int32_t)h, 0, hi);
+      store_bytes(dal, v, h, h + hi);
+    }
+    if (o0 == o1) continue;
+    const uint32_t plen = IS_KEY ? (o1 - o0) - ((uint32_t)me.z - me.x) : 0u;
+    for (uint32_t q = (o0 + h + 15) >> 4; 16 * q < o1 + h; q++) {
+      const int32_t t0 = (int32_t)(16 * q) - (int32_t)h;  // >= o0 >= 0
+      const uint32_t ut0 = (uint32_t)t0;
+      if (ut0 + 16 > L) {  // trailing partial chunk
+        const uint4 v = assemble<IS_KEY>(slot, sh, meta, e, base_pos, t0, ut0, L);
+        store_bytes(dal + 16 * q, v, 0, L - ut0);
+        continue;
       }
-      const uint32_t u = t - o0;
-      uint32_t src, rend;
-      if (!IS_KEY) {
-        src = me.z + u;
-        rend = o1;
+      uint4 v;
+      const uint32_t u0 = ut0 - o0;
+      if (ut0 + 16 <= o1 && (!IS_KEY || u0 >= plen)) {        // inside the value / key diff
+        v = lds_u128(slot, sh + (IS_KEY ? me.x + (u0 - plen) : me.z + u0));
+      } else if (IS_KEY && u0 + 16 <= plen) {                  // inside the baseKey prefix
+        v = lds_u128(slot, sh + base_pos + u0);
       } else {
-        const uint32_t plen = (o1 - o0) - ((uint32_t)me.z - me.x);
-        if (u < plen) {
-          src = base_pos + u;
-          rend = o0 + plen;
-        } else {
-          src = me.x + (u - plen);
-          rend = o1;
-        }
+        v = assemble<IS_KEY>(slot, sh, meta, e, base_pos, t0, ut0, ut0 + 16);
       }
-      if (rend > hi) rend = hi;
-      const uint32_t a = t - (uint32_t)t0;  // chunk byte of this run's start (0..15)
-      // window whose byte a is block byte src (slot has >= 16 B of addressable LDS before sh)
-      const uint4 w = lds_u128(slot - 16, sh + src + 16 - a);
+      *reinterpret_cast<uint4*>(dal + 16 * q) = v;
+    }
+  }
+}
+
+// Bytes [lo, hi) of the 16-B chunk that starts at stream byte t0, for a stream whose entry e
+// occupies [o(e), o(e+1)) and comes from block bytes starting at src(e) (no prefixes: keys of
+// a plen == 0 block or values).  Entry e must contain lo.  One window + blend per entry run.
+template <int OCOL, int SCOL>
+__device__ __forceinline__ uint4 assemble_plain(const uint8_t* slot, uint32_t sh,
+                                                const uint16_t* meta, uint32_t e, int32_t t0,
+                                                uint32_t lo, uint32_t hi) {
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  uint32_t t = lo;
+  uint32_t o0 = meta[4 * e + OCOL], s0 = meta[4 * e + SCOL];
+  while (t < hi) {
+    const uint32_t o1 = meta[4 * (e + 1) + OCOL];
+    const uint32_t rend = o1 < hi ? o1 : hi;
+    if (rend > t) {
+      const uint32_t a = t - (uint32_t)t0;
+      const uint4 w = lds_u128(slot - 16, sh + s0 + (t - o0) + 16 - a);
       blend16(acc, w, a, rend - (uint32_t)t0);
       t = rend;
     }
-    if (lo == (uint32_t)t0 && hi == (uint32_t)t0 + 16) {
-      *reinterpret_cast<uint4*>(dal + 16 * c) = acc;
-    } else {  // stream edge: only this block's bytes (neighbours own the rest of the chunk)
-      const uint32_t words[4] = {acc.x, acc.y, acc.z, acc.w};
-      for (uint32_t i = lo - (uint32_t)t0; i < hi - (uint32_t)t0; i++)
-        dal[16 * c + i] = (uint8_t)(words[i >> 2] >> (8 * (i & 3)));
-    }
+    e++;
+    o0 = o1;
+    s0 = meta[4 * e + SCOL];
+  }
+  return acc;
+}
+
+// One stream (OCOL = output-offset column, SCOL = block-position column) of one block,
+// lane-per-entry: interior chunks are one window + one aligned dwordx4 store; the chunk that
+// crosses the entry's end is assembled; the stream's partial head / tail chunks are stored
+// byte-wise (the neighbouring blocks own the other bytes of those chunks).
+template <int OCOL, int SCOL>
+__device__ __forceinline__ void emit_plain(uint8_t* dst, uint32_t L, const uint8_t* slot,
+                                           uint32_t sh, const uint16_t* meta, uint32_t e,
+                                           uint32_t o0, uint32_t o1, uint32_t s0, uint32_t h) {
+  uint8_t* dal = dst - h;  // chunk q covers stream bytes [16q - h, 16q - h + 16)
+  if (e == 0 && h != 0) {
+    const uint32_t hi = (16 - h < L) ? 16 - h : L;
+    const uint4 v = assemble_plain<OCOL, SCOL>(slot, sh, meta, 0, -(int32_t)h, 0, hi);
+    store_bytes(dal, v, h, h + hi);
+  }
+  // chunks fully inside [o0, o1)
+  const uint32_t qa = (o0 + h + 15) >> 4, qb = (o1 + h) >> 4;  // [qa, qb)
+  for (uint32_t q = qa; q < qb; q++)
+    *reinterpret_cast<uint4*>(dal + 16 * q) = lds_u128(slot, sh + s0 + (16 * q - h - o0));
+  // the chunk starting inside [o0, o1) that crosses o1 (or the stream end)
+  const uint32_t qc = qb > qa ? qb : qa;
+  const int32_t t0 = (int32_t)(16 * qc) - (int32_t)h;
+  if ((uint32_t)t0 < o1 && t0 >= (int32_t)o0) {
+    const uint32_t hi = ((uint32_t)t0 + 16 < L) ? (uint32_t)t0 + 16 : L;
+    const uint4 v = assemble_plain<OCOL, SCOL>(slot, sh, meta, e, t0, (uint32_t)t0, hi);
+    if (hi == (uint32_t)t0 + 16) *reinterpret_cast<uint4*>(dal + 16 * qc) = v;
+    else store_bytes(dal + 16 * qc, v, 0, hi - (uint32_t)t0);
   }
 }
 
@@ -553,7 +640,7 @@ __global__ void __launch_bounds__(WPB * 64) decode_kernel(DecodeParams p) {
     const uint32_t b = tile * WPB + wv;
     const bool valid = b < p.nblk;
     WalkResult w{0, 0, 0, LSMGPU_BLK_OK, 0, 0};
-    bool fast = false;
+    bool fast = false, any_plen = false;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's DMA has landed
     if (valid) {
       if (ref.off + ref.len > p.data_len) {
@@ -567,7 +654,7 @@ __global__ void __launch_bounds__(WPB * 64) decode_kernel(DecodeParams p) {
           const SpecResult r = walk_spec(slot, ref.sh, ref.len, meta, MAXE, lane);
           if (r.n <= (uint32_t)MAXE) {
             wave_lds_fence();
-            w = finish_meta(slot, ref.sh, r, meta, lane);
+            w = finish_meta(slot, ref.sh, r, meta, lane, any_plen);
             fast = (w.K <= 0xffffu) && (w.V <= 0xffffu);
           } else {  // too many entries for the metadata: count on the global path
             w = walk_block(GlobalSrc{p.data + ref.off}, ref.len, meta, 0, false, lane);
@@ -647,13 +734,20 @@ __global__ void __launch_bounds__(WPB * 64) decode_kernel(DecodeParams p) {
           emit_slow(p, p.data + ref.off, w.n, ex.n, ex.k, ex.v, ref.off, lane);
         } else {
           const uint32_t en = ex.n, ek = ex.k, evv = ex.v;
-          // per-entry offsets / view records: lane e handles entry e (coalesced stores)
+          const bool keys_plain = !any_plen;
+          const uint32_t hk = (uint32_t)(reinterpret_cast<uintptr_t>(p.key_data + ek) & 15u);
+          const uint32_t hv = (uint32_t)(reinterpret_cast<uintptr_t>(p.val_data + evv) & 15u);
+          // lane e: entry e's offsets / view record and the stream chunks starting inside it
           for (uint32_t e = lane; e < w.n; e += kWave) {
             const ushort4 me = *reinterpret_cast<const ushort4*>(meta + 4 * e);
             const ushort4 mn = *reinterpret_cast<const ushort4*>(meta + 4 * e + 4);
             if (mat) {
               if (p.key_end) p.key_end[en + e] = ek + mn.y;
               if (p.val_end) p.val_end[en + e] = evv + mn.w;
+              if (p.val_data)
+                emit_plain<3, 2>(p.val_data + evv, w.V, slot, ref.sh, meta, e, me.w, mn.w, me.z, hv);
+              if (p.key_data && keys_plain)
+                emit_plain<1, 0>(p.key_data + ek, w.K, slot, ref.sh, meta, e, me.y, mn.y, me.x, hk);
             }
             if (view) {
               const uint32_t klen = (uint32_t)me.z - me.x, vlen = (uint32_t)mn.w - me.w;
@@ -661,12 +755,8 @@ __global__ void __launch_bounds__(WPB * 64) decode_kernel(DecodeParams p) {
                                ((uint64_t)vlen << 48);
             }
           }
-          if (mat) {
-            if (p.key_data)
-              gather_stream<true>(p.key_data + ek, w.K, slot, ref.sh, meta, w.n, w.base_pos, lane);
-            if (p.val_data)
-              gather_stream<false>(p.val_data + evv, w.V, slot, ref.sh, meta, w.n, 0, lane);
-          }
+          if (mat && p.key_data && !keys_plain)  // prefix-compressed keys (plen > 0)
+            emit_stream<true>(p.key_data + ek, w.K, slot, ref.sh, meta, w.n, w.base_pos, lane);
         }
       }
     }
@@ -729,7 +819,7 @@ static hipError_t launch_cfg(const DecodeParams& p, int num_cus, hipStream_t s,
 
 hipError_t launch_decode(const DecodeParams& p, uint32_t max_blk_len, int num_cus,
                          hipStream_t s, uint64_t* waves_launched) {
-  if (max_blk_len <= 4096) return launch_cfg<4096, 128, 8>(p, num_cus, s, waves_launched);
+  if (max_blk_len <= 4096) return launch_cfg<4096, 128, 4>(p, num_cus, s, waves_launched);
   if (max_blk_len <= 8192) return launch_cfg<8192, 256, 4>(p, num_cus, s, waves_launched);
   if (max_blk_len <= 16384) return launch_cfg<16384, 512, 2>(p, num_cus, s, waves_launched);
   // 32 KiB slot; larger blocks run the global-memory path inside the same kernel

@@ -229,9 +229,11 @@ def _be32(b, o):
 
 
 def OpenTable(path_or_bytes, loading_mode: int = MEMORY_MAP, codec: Optional[Codec] = None,  # noqa: N802
-              file_id: Optional[int] = None) -> Table:
+              file_id: Optional[int] = None, decoder=None) -> Table:
     """table.go:88-144.  Accepts a path (the file is deleted by DecrRef at ref 0, like Go) or
-    the table bytes themselves."""
+    the table bytes themselves.  `decoder(data, blk_off, blk_len)` defaults to the HIP batch
+    decode (Codec.decode_host); tests may inject another decoder to exercise this host logic
+    without a GPU."""
     t = Table()
     t.loading_mode = loading_mode
     if isinstance(path_or_bytes, (bytes, bytearray, memoryview)):
@@ -253,7 +255,9 @@ def OpenTable(path_or_bytes, loading_mode: int = MEMORY_MAP, codec: Optional[Cod
                 raw = f.read()
     t.raw = raw
     t.table_size = len(raw)
-    _read_index(t, codec or default_codec())
+    if decoder is None:
+        decoder = (codec or default_codec()).decode_host
+    _read_index(t, decoder)
     it = t.NewIterator(False)
     it.Rewind()
     if it.Valid():
@@ -267,15 +271,15 @@ def OpenTable(path_or_bytes, loading_mode: int = MEMORY_MAP, codec: Optional[Cod
     return t
 
 
-def _read_index(t: Table, codec: Codec) -> None:
+def _read_index(t: Table, decoder) -> None:
     """table.go:177-269 readIndex: tail parse, every block decoded on the GPU, first keys
     (with the plen==0 assertion, table.go:239), then the sort by key (table.go:267)."""
     raw = t.raw
     off, ln, bo, bl = parse_index(raw)
     t.bloom_json = raw[bo: bo + bl]
     data_end = int(off[-1] + ln[-1]) if off.size else 0
-    t.dec = codec.decode_host(np.frombuffer(raw, np.uint8)[: max(data_end, 1)] if data_end
-                              else np.zeros(16, np.uint8), off, ln)
+    t.dec = decoder(np.frombuffer(raw, np.uint8)[:data_end] if data_end
+                    else np.zeros(16, np.uint8), off, ln)
     kos = []
     for b in range(off.size):
         o, n = int(off[b]), int(ln[b])

@@ -1,0 +1,174 @@
+"""y/iterator_test.go (MergeIterator over an in-memory SimpleIterator) + y helpers + bloom tail."""
+import bisect
+import json
+import base64
+import time
+
+import pytest
+
+from lsmdb_amd import bloom
+from lsmdb_amd.y import (MergeIterator, ValueStruct, compare_keys, key_with_ts, parse_key,
+                         parse_ts, same_key, AssertionFailed)
+import kat_defs as K
+
+close_count = [0]
+
+
+class SimpleIterator:
+    """y/iterator_test.go:11-80"""
+
+    def __init__(self, keys, vals, reversed_):
+        ts = int(time.time())
+        self.keys = [key_with_ts(k.encode(), ts) for k in keys]
+        self.vals = [v.encode() for v in vals]
+        self.idx = -1
+        self.reversed = reversed_
+
+    def Close(self):
+        close_count[0] += 1
+
+    def Next(self):
+        self.idx += -1 if self.reversed else 1
+
+    def Rewind(self):
+        self.idx = len(self.keys) - 1 if self.reversed else 0
+
+    def Seek(self, key):
+        key = key_with_ts(key, 0)
+        n = len(self.keys)
+        if not self.reversed:
+            lo, hi = 0, n
+            while lo < hi:
+                m = (lo + hi) // 2
+                if compare_keys(self.keys[m], key) >= 0:
+                    hi = m
+                else:
+                    lo = m + 1
+            self.idx = lo
+        else:
+            lo, hi = 0, n
+            while lo < hi:
+                m = (lo + hi) // 2
+                if compare_keys(self.keys[n - 1 - m], key) <= 0:
+                    hi = m
+                else:
+                    lo = m + 1
+            self.idx = n - 1 - lo
+
+    def Key(self):
+        return self.keys[self.idx]
+
+    def Value(self):
+        return ValueStruct(value=self.vals[self.idx], user_meta=55, meta=0)
+
+    def Valid(self):
+        return 0 <= self.idx < len(self.keys)
+
+
+def get_all(it):
+    ks, vs = [], []
+    while it.Valid():
+        ks.append(parse_key(it.Key()).decode())
+        vs.append(it.Value().value.decode())
+        it.Next()
+    return ks, vs
+
+
+def close_and_check(it, expected):
+    close_count[0] = 0
+    it.Close()
+    assert close_count[0] == expected
+
+
+def four(rev):
+    return [SimpleIterator(["1", "3", "7"], ["a1", "a3", "a7"], rev),
+            SimpleIterator(["2", "3", "5"], ["b2", "b3", "b5"], rev),
+            SimpleIterator(["1"], ["c1"], rev),
+            SimpleIterator(["1", "7", "9"], ["d1", "d7", "d9"], rev)]
+
+
+def test_simple_iterator():
+    it = SimpleIterator(["1", "2", "3"], ["v1", "v2", "v3"], False)
+    it.Rewind()
+    assert get_all(it) == (["1", "2", "3"], ["v1", "v2", "v3"])
+    close_and_check(it, 1)
+
+
+@pytest.mark.parametrize("rev", [False, True])
+def test_merge_single(rev):
+    it = MergeIterator([SimpleIterator(["1", "2", "3"], ["v1", "v2", "v3"], rev)], rev)
+    it.Rewind()
+    k, v = get_all(it)
+    exp_k, exp_v = ["1", "2", "3"], ["v1", "v2", "v3"]
+    assert (k, v) == ((exp_k[::-1], exp_v[::-1]) if rev else (exp_k, exp_v))
+    close_and_check(it, 1)
+
+
+def test_merge_more():
+    it = MergeIterator(four(False), False)
+    it.Rewind()
+    assert get_all(it) == (["1", "2", "3", "5", "7", "9"], ["a1", "b2", "a3", "b5", "a7", "d9"])
+    close_and_check(it, 4)
+
+
+def test_merge_nested():
+    m1 = MergeIterator([SimpleIterator(["1", "2", "3"], ["v1", "v2", "v3"], False)], False)
+    m2 = MergeIterator([m1], False)
+    m2.Rewind()
+    assert get_all(m2) == (["1", "2", "3"], ["v1", "v2", "v3"])
+    close_and_check(m2, 1)
+
+
+def test_merge_seek():
+    it = MergeIterator(four(False), False)
+    it.Seek(b"4")
+    assert get_all(it) == (["5", "7", "9"], ["b5", "a7", "d9"])
+    close_and_check(it, 4)
+
+
+def test_merge_seek_reversed():
+    it = MergeIterator(four(True), True)
+    it.Seek(b"5")
+    assert get_all(it) == (["5", "3", "2", "1"], ["b5", "a3", "b2", "a1"])
+    close_and_check(it, 4)
+
+
+@pytest.mark.parametrize("rev,k", [(False, b"f"), (True, b"0")])
+def test_merge_seek_invalid(rev, k):
+    it = MergeIterator(four(rev), rev)
+    it.Seek(k)
+    assert not it.Valid()
+    close_and_check(it, 4)
+
+
+@pytest.mark.parametrize("meta,um,exp,val,enc,size", K.VS_KATS)
+def test_valuestruct(meta, um, exp, val, enc, size):
+    vs = ValueStruct(meta=meta, user_meta=um, expires_at=exp, value=val)
+    assert vs.encoded_size() == size
+    if enc is not None:
+        assert vs.encode() == enc
+        d = ValueStruct.decode(enc)
+        assert (d.meta, d.user_meta, d.expires_at, d.value) == (meta, um, exp, val)
+
+
+def test_key_helpers():
+    k = key_with_ts(b"abc", 7)
+    assert len(k) == 11 and parse_ts(k) == 7 and parse_key(k) == b"abc"
+    assert compare_keys(key_with_ts(b"a", 5), key_with_ts(b"b", 1)) < 0
+    assert compare_keys(key_with_ts(b"a", 5), key_with_ts(b"a", 1)) < 0  # newer ts sorts first
+    assert same_key(key_with_ts(b"a", 5), key_with_ts(b"a", 1))
+    with pytest.raises(AssertionFailed):
+        compare_keys(b"short", b"alsoshort")
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 100, 10000, 519540])
+def test_bloom_tail_shape(n):
+    raw = bloom.bloom_tail(n)
+    doc = json.loads(raw)
+    assert list(doc) == ["FilterSet", "SetLocs"]
+    fs = base64.b64decode(doc["FilterSet"])
+    size, locs = bloom.bbloom_params(float(n))
+    assert len(fs) * 8 == size and size >= 512 and (size & (size - 1)) == 0
+    assert doc["SetLocs"] == locs
+    assert all(b == 0xFF for b in fs)
+    assert bloom.may_contain(raw, b"anything")
