@@ -75,6 +75,12 @@ def build_device_sst(codec, torch, dev, cfg: int, target_bytes: int, shard: int)
                 d_ve=d_ve, max_len=int(lens.max()), offs=offs, lens=lens)
 
 
+def _lib_sha256():
+    import hashlib
+    with open(os.path.join(ROOT, "lsmdb_amd", "liblsmgpu.so"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def algorithmic_bytes(w, mode: int) -> tuple[int, int]:
     """(read, write) bytes one decode launch must move."""
     read = w["data_len"] + 8 * w["nblocks"]            # block bytes + (off, len) per block
@@ -227,7 +233,8 @@ def main():
         try:
             with open(tp) as f:
                 tj = json.load(f)
-            if tj.get("workload_bytes") == w["data_len"] and tj.get("mode") == mode:
+            if (tj.get("workload_bytes") == w["data_len"] and tj.get("mode") == mode
+                    and tj.get("lib_sha256") == _lib_sha256()):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
