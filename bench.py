@@ -129,6 +129,26 @@ def check_round_trip(torch, w, bufs) -> str:
     return "ok" if ok else "MISMATCH"
 
 
+def reduce_over_ranks(dist, torch, dev, wall: float, parity: str,
+                      shard_bytes: int) -> tuple[float, str, int]:
+    """MAX of the timed wall clock, AND of the parity verdicts and SUM of the shard bytes over
+    all ranks (the only collectives; the decode itself exchanges nothing)."""
+    if dist is None:
+        return wall, parity, shard_bytes
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    p = torch.tensor([1.0 if parity == "ok" else 0.0], dtype=torch.float64, device=dev)
+    dist.all_reduce(p, op=dist.ReduceOp.MIN)
+    b = torch.tensor([shard_bytes], dtype=torch.int64, device=dev)
+    dist.all_reduce(b, op=dist.ReduceOp.SUM)
+    return float(t.item()), ("ok" if p.item() == 1.0 else "MISMATCH"), int(b.item())
+
+
+def aggregate_gibs(total_bytes: int, ms_per_step: float) -> float:
+    """Whole-job input GiB/s: the bytes all ranks decode per step / the slowest rank's step."""
+    return total_bytes / (ms_per_step / 1e3) / (1 << 30)
+
+
 def cpu_baseline(torch, w, seconds: float) -> dict:
     """The oracle (C restatement of blockIterator.Next/parseKV) on a bounded sample of the same
     blocks, multi-threaded over block ranges on the host cores."""
@@ -213,18 +233,10 @@ def main():
                 "frac": round((vr + vw) / (vk / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
         del vbufs
 
-    # max over ranks of the timed wall clock
-    if dist is not None:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
-        p = torch.tensor([1.0 if parity == "ok" else 0.0], dtype=torch.float64, device=dev)
-        dist.all_reduce(p, op=dist.ReduceOp.MIN)
-        parity = "ok" if p.item() == 1.0 else "MISMATCH"
+    wall, parity, total_bytes = reduce_over_ranks(dist, torch, dev, wall, parity, w["data_len"])
 
     ms_per_step = wall / args.steps * 1e3
-    total_bytes = w["data_len"] * world
-    value = total_bytes / (ms_per_step / 1e3) / (1 << 30)
+    value = aggregate_gibs(total_bytes, ms_per_step)
     rd, wr = algorithmic_bytes(w, mode)
     achieved = (rd + wr) / (kms_mean / 1e3) / 1e9
     traffic = None
