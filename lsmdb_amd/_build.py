@@ -26,6 +26,8 @@ def build_lib(force: bool = False, verbose: bool = True) -> str:
         return LIB
     cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
            "-o", LIB] + [os.path.join(CSRC, s) for s in SOURCES]
+    if os.environ.get("LSMGPU_BUILD_STAMPS"):  # diagnostic build: per-phase s_memtime stamps
+        cmd.insert(1, "-DLSMGPU_STAMPS")
     if verbose:
         print("[build]", " ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=CSRC)

@@ -2,22 +2,25 @@
 // (table/iterator.go:93-135) driven over every block of a batch (Iterator.seekToFirst/next,
 // iterator.go:201-217,301-326).
 //
-// Work decomposition (see DESIGN.md, "decode kernel"):
+// Work decomposition (DESIGN.md, "decode kernel"):
 //   tile   = WPB consecutive blocks, one per wave of a workgroup; a persistent, fully
 //            resident grid walks the tiles round-robin (tile = blockIdx.x + k * gridDim.x)
-//   stage  : each wave's block -> its LDS slot with 16-B loads; the NEXT tile's loads are
-//            issued into registers before the current tile waits on its prefix (the wait is
-//            hidden behind HBM latency), and land in LDS after the current emit
-//   walk   : the serial header chain (pos += 10 + klen + vlen) in LDS on the VALU (the CU's
-//            single scalar unit would serialise every wave's chain), recording per entry
-//            {key pos, key out offset, value pos, value out offset}
-//   prefix : tile aggregates -> groups of 64 tiles; the last tile of a group to arrive
-//            scans the group, looks back over earlier GROUPS and publishes every member's
-//            exclusive output base (8-B {tag, value} granules, agent scope)
-//   emit   : per-entry end offsets (coalesced u32), key and value streams written as
-//            aligned 16-B chunks gathered from LDS (a chunk may blend several entries' runs)
-// Blocks larger than the slot, or with more entries than the metadata holds, take a
-// global-memory path with identical semantics.
+//   stage  : each wave's block -> an LDS slot by LDS-DMA (global_load_lds_dwordx4); with
+//            NS = 3 slots the next tile's block is in flight during the current iteration
+//   walk   : the serial header chain (pos += 10 + klen + vlen), speculated a whole run of
+//            equal-size entries per LDS round trip; per entry {header pos, key offset}
+//   prefix : tile aggregates -> groups of 64 tiles; the last tile of a group to arrive scans
+//            the group, looks back over earlier GROUPS and publishes every member's exclusive
+//            output base (8-B {tag, value} granules, agent scope)
+//   emit   : SOFTWARE-PIPELINED one tile behind the walk: iteration k walks tile k and
+//            publishes its aggregate, then waits for tile k-1's base (published a whole
+//            iteration earlier) and writes tile k-1's streams.  Lanes map to aligned 16-B
+//            output chunks (J lanes per entry); a chunk is one or two unaligned LDS windows
+//            blended at the entry boundary and one dwordx4 store; the stream's partial head /
+//            tail chunks are scattered byte-wise (the neighbouring blocks own the rest).
+// Blocks larger than the slot, with more entries than the metadata holds, or with prefix-
+// compressed keys (plen > 0: never written by table.Builder) take a global-memory
+// path with identical semantics.
 #include <cstdio>
 #include <cstdlib>
 
@@ -35,14 +38,12 @@ struct LdsSrc {
   const uint8_t* slot;  // 16-B aligned LDS slot (block byte 0 at slot + sh)
   uint32_t sh;
   __device__ __forceinline__ Hdr hdr(uint32_t pos) const {
-    const uint32_t p = sh + pos;
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(slot + (p & ~3u));
-    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-    const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, p & 3u);  // plen:klen (BE)
-    const uint32_t x1 = __builtin_amdgcn_alignbyte(w2, w1, p & 3u);  // vlen:..   (BE)
+    // one unaligned ds_read_b64 (gfx950 runs in unaligned-access mode): plen klen vlen prev.hi
+    uint2 w;
+    __builtin_memcpy(&w, slot + sh + pos, 8);
     // v_perm byte selects: BE u16 -> u32
-    return Hdr{__builtin_amdgcn_perm(0u, x0, 0x0c0c0001u), __builtin_amdgcn_perm(0u, x0, 0x0c0c0203u),
-               __builtin_amdgcn_perm(0u, x1, 0x0c0c0001u)};
+    return Hdr{__builtin_amdgcn_perm(0u, w.x, 0x0c0c0001u), __builtin_amdgcn_perm(0u, w.x, 0x0c0c0203u),
+               __builtin_amdgcn_perm(0u, w.y, 0x0c0c0001u)};
   }
 };
 struct GlobalSrc {
@@ -55,14 +56,12 @@ struct GlobalSrc {
 };
 
 struct WalkResult {
-  uint32_t n, K, V, status, base_pos, end_pos;
+  uint32_t n, K, V, status;
 };
 
-// The blockIterator forward walk.  `meta` (LDS, stride 4 u16) gets {ks, ko, vs, vo} for
-// entries < maxe when record is set.  Values are identical in every lane (VALU, no SALU).
-template <class Src>
-__device__ __forceinline__ WalkResult walk_block(const Src& src, uint32_t len, uint16_t* meta,
-                                                 uint32_t maxe, bool record, uint32_t lane) {
+// The blockIterator forward walk over global memory (count only; oversize blocks).
+// Values are identical in every lane.
+__device__ __forceinline__ WalkResult walk_block(const GlobalSrc& src, uint32_t len) {
   uint32_t pos = 0, n = 0, K = 0, V = 0, st = LSMGPU_BLK_OK, base_pos = 0;
   bool have_base = false;
   for (;;) {
@@ -77,75 +76,84 @@ __device__ __forceinline__ WalkResult walk_block(const Src& src, uint32_t len, u
       have_base = true;
     }
     if (base_pos + h.plen > len) { st = LSMGPU_BLK_PREFIX_OOB; break; }
-    const uint32_t ks = pos;
     pos += h.klen;                                           // iterator.go:101
     if (pos + h.vlen > len) { st = LSMGPU_BLK_VALUE_OVERFLOW; break; }  // iterator.go:103
-    const uint32_t vs = pos;
     pos += h.vlen;                                           // iterator.go:109
-    if (record && n < maxe && lane == 0) {
-      ushort4 m = make_ushort4((uint16_t)ks, (uint16_t)K, (uint16_t)vs, (uint16_t)V);
-      *reinterpret_cast<ushort4*>(meta + 4 * n) = m;
-    }
     K += h.plen + h.klen;
     V += h.vlen;
     n++;
   }
-  return WalkResult{n, K, V, st, base_pos, pos};
+  return WalkResult{n, K, V, st};
 }
 
-__device__ __forceinline__ uint32_t wave_scan_incl32(uint32_t v, uint32_t lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t x = __shfl_up(v, o);
-    if (lane >= (uint32_t)o) v += x;
-  }
+// ---- wave primitives: DPP row_shr inside each 16-lane row, the four rows combined through
+// v_readlane (scalar).  (No row_bcast: its row-masked forms are not relied on here.)
+__device__ __forceinline__ uint32_t readlane(uint32_t v, uint32_t l) {
+  return __builtin_amdgcn_readlane(v, l);
+}
+__device__ __forceinline__ uint32_t row_incl_add(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true);   // row_shr:8
   return v;
 }
+// inclusive scan over the wave; `total` = the wave's sum (uniform)
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t v, uint32_t lane, uint32_t& total) {
+  v = row_incl_add(v);
+  const uint32_t r0 = readlane(v, 15), r1 = r0 + readlane(v, 31), r2 = r1 + readlane(v, 47);
+  total = r2 + readlane(v, 63);
+  const uint32_t row = lane >> 4;
+  return v + (row == 0 ? 0u : row == 1 ? r0 : row == 2 ? r1 : r2);
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {  // uniform result
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true));
+  return max(max(readlane(v, 15), readlane(v, 31)), max(readlane(v, 47), readlane(v, 63)));
+}
 
-// Speculative parallel walk of a block held in LDS, exactly equivalent to walk_block.
+// ---- speculative walk of a block held in LDS, exactly equivalent to the iterator's walk.
 // The chain pos_{e+1} = pos_e + 10 + klen_e + vlen_e is serial, but SST entries of a block
 // mostly share one size: each round lane i reads the header guessed at pos + i*stride, a
 // ballot finds the first lane whose entry stops the iterator (end, terminator, error) or
 // whose size differs from the stride, and every lane before it is a confirmed entry.  A
-// round therefore advances over a whole run of equal-size entries with ONE LDS round trip;
-// a size change simply starts the next round at the mismatching entry's successor.
+// round therefore advances over a whole run of equal-size entries with ONE LDS round trip.
+// meta[e] = header pos | klen << 16 for e < maxe.
 struct SpecResult {
-  uint32_t n, status, base_pos, end_pos;
+  uint32_t n, status, stop;  // stop = position just after the last entry (its successor's header)
+  bool any_plen;
+  uint32_t rounds;
 };
-__device__ __forceinline__ uint32_t readlane(uint32_t v, uint32_t l) {
-  return __builtin_amdgcn_readlane(v, l);
-}
-// Status of the iterator at a position where no entry was confirmed (walk_block's rules).
-__device__ __forceinline__ SpecResult stop_at(const LdsSrc& src, uint32_t pf, uint32_t len,
-                                              uint32_t n, uint32_t base_pos, bool first) {
-  uint32_t st = LSMGPU_BLK_OK, end = pf;
-  if (pf < len) {                                          // else: pos >= len, io.EOF
-    if (len - pf < 10) {
-      st = LSMGPU_BLK_TRUNC_HEADER;
-    } else {
-      const Hdr h = src.hdr(pf);
-      if ((h.klen | h.plen) == 0) end = pf + 10;            // terminator
-      else if (first && h.plen != 0) st = LSMGPU_BLK_FIRST_PLEN;
-      else if (base_pos + h.plen > len) st = LSMGPU_BLK_PREFIX_OOB;
-      else st = LSMGPU_BLK_VALUE_OVERFLOW;                  // p + 10 + klen + vlen > len
-    }
-  }
-  return SpecResult{n, st, base_pos, end};
+// Status of the iterator at a position where no entry was confirmed.
+__device__ __forceinline__ uint32_t stop_status(const LdsSrc& src, uint32_t pf, uint32_t len,
+                                                uint32_t base_pos, bool first) {
+  if (pf >= len) return LSMGPU_BLK_OK;                    // io.EOF (iterator.go:115-118)
+  if (len - pf < 10) return LSMGPU_BLK_TRUNC_HEADER;
+  const Hdr h = src.hdr(pf);
+  if ((h.klen | h.plen) == 0) return LSMGPU_BLK_OK;       // terminator (iterator.go:124-127)
+  if (first && h.plen != 0) return LSMGPU_BLK_FIRST_PLEN; // iterator.go:131
+  if (base_pos + h.plen > len) return LSMGPU_BLK_PREFIX_OOB;
+  return LSMGPU_BLK_VALUE_OVERFLOW;                       // iterator.go:103-106
 }
 
 __device__ __forceinline__ SpecResult walk_spec(const uint8_t* slot, uint32_t sh, uint32_t len,
-                                                uint16_t* meta, uint32_t maxe, uint32_t lane) {
+                                                uint32_t* meta, uint32_t maxe, uint32_t lane) {
   const LdsSrc src{slot, sh};
   // first entry (uniform): defines baseKey (iterator.go:129-133) and the first stride guess
-  if (len < 10) return stop_at(src, 0, len, 0, 10, true);
+  if (len < 10) return SpecResult{0, stop_status(src, 0, len, 10, true), 0, false, 0};
   const Hdr h0 = src.hdr(0);
   const uint32_t base_pos = 10;
   const uint32_t sz0 = 10 + h0.klen + h0.vlen;
-  if ((h0.klen | h0.plen) == 0 || h0.plen != 0 || base_pos + h0.plen > len || sz0 > len)
-    return stop_at(src, 0, len, 0, base_pos, true);
-  if (lane == 0 && maxe > 0) meta[0] = 0;
+  if ((h0.klen | h0.plen) == 0 || h0.plen != 0 || sz0 > len)
+    return SpecResult{0, stop_status(src, 0, len, base_pos, true), 0, false, 0};
+  if (lane == 0 && maxe > 0) meta[0] = h0.klen << 16;
   uint32_t pos = sz0, stride = sz0, n = 1;
+  bool any_plen = false;
+  uint32_t rounds = 0;
   for (;;) {
+    rounds++;
     // lane i checks the entry guessed at pos + i*stride (branch-free)
     const uint32_t p = pos + lane * stride;
     const bool has_hdr = p + 10 <= len;
@@ -153,80 +161,104 @@ __device__ __forceinline__ SpecResult walk_spec(const uint8_t* slot, uint32_t sh
     const uint32_t sz = 10 + h.klen + h.vlen;
     const bool bad = !has_hdr || (h.klen | h.plen) == 0 || base_pos + h.plen > len || p + sz > len;
     const uint64_t any = __ballot(bad || sz != stride);
-    if (any == 0) {  // 64 entries of exactly `stride` bytes
-      if (n + lane < maxe) meta[4 * (n + lane)] = (uint16_t)p;
-      n += 64;
+    const uint32_t f = any ? (uint32_t)__builtin_ctzll(any) : 64u;
+    const bool fbad = f < 64 && ((__ballot(bad) >> f) & 1ull);
+    const uint32_t m = f + ((f < 64 && !fbad) ? 1u : 0u);  // confirmed entries: lanes [0, m)
+    const bool conf = lane < m;
+    if (conf && n + lane < maxe) meta[n + lane] = p | (h.klen << 16);
+    any_plen = any_plen || (__ballot(conf && h.plen != 0) != 0);
+    n += m;
+    if (f == 64) {  // 64 entries of exactly `stride` bytes
       pos += 64 * stride;
       continue;
     }
-    const uint32_t f = (uint32_t)__builtin_ctzll(any);
-    const bool fbad = (__ballot(bad) >> f) & 1ull;
-    const uint32_t m = f + (fbad ? 0u : 1u);  // confirmed entries: lanes [0, m)
-    if (lane < m && n + lane < maxe) meta[4 * (n + lane)] = (uint16_t)p;
-    n += m;
     const uint32_t pf = readlane(p, f);
-    if (fbad) return stop_at(src, pf, len, n, base_pos, false);
+    if (fbad) return SpecResult{n, stop_status(src, pf, len, base_pos, false), pf, any_plen, rounds};
     const uint32_t szf = readlane(sz, f);  // entry f has another size: continue after it
     pos = pf + szf;
     if (f == 0) stride = szf;  // the guess failed at once: adopt the new size
   }
 }
 
-// After walk_spec: lane e turns row e's header position into {ks, ko, vs, vo} (wave scans of
-// the key / value output sizes) and row n into the totals sentinel.  Requires n <= maxe.
-__device__ __forceinline__ WalkResult finish_meta(const uint8_t* slot, uint32_t sh,
-                                                  const SpecResult& r, uint16_t* meta,
-                                                  uint32_t lane, bool& any_plen) {
-  const LdsSrc src{slot, sh};
-  uint32_t K = 0, V = 0;
-  any_plen = false;
+// Per-block emit plan (uniform).  kind: 0 nothing to write, 1 LDS fast path, 2 global path.
+struct Plan {
+  uint32_t n, K, V, status;
+  uint32_t off, len, sh;
+  uint32_t kind;
+  uint32_t jk, jv;       // log2(lanes per entry) of the key / value streams
+};
+
+// After walk_spec: meta[e] := header pos | key offset << 16 (wave scan of klen), sentinel
+// meta[n] = stop | K << 16; derives the stream sizes, lanes-per-entry and the 2-run flags.
+// Requires n <= maxe (meta holds maxe + 2 words).
+__device__ __forceinline__ void finish_meta(uint32_t* meta, const SpecResult& r, uint32_t lane,
+                                            Plan& pl) {
+  if (lane == 0) meta[r.n] = r.stop;  // klen field 0: the walk's successor position
+  wave_lds_fence();
+  uint32_t K = 0, kmax = 0, vmax = 0;
   for (uint32_t e0 = 0; e0 < r.n; e0 += kWave) {
     const uint32_t e = e0 + lane;
     const bool on = e < r.n;
-    uint32_t hp = 0;
-    Hdr h{0, 0, 0};
-    if (on) {
-      hp = meta[4 * e];
-      h = src.hdr(hp);
-    }
-    const uint32_t kl = on ? h.plen + h.klen : 0u, vl = on ? h.vlen : 0u;
-    any_plen = any_plen || __any(on && h.plen != 0);
-    const uint32_t ki = wave_scan_incl32(kl, lane), vi = wave_scan_incl32(vl, lane);
-    if (on)
-      *reinterpret_cast<ushort4*>(meta + 4 * e) =
-          make_ushort4((uint16_t)(hp + 10), (uint16_t)(K + ki - kl), (uint16_t)(hp + 10 + h.klen),
-                       (uint16_t)(V + vi - vl));
-    K += __shfl(ki, 63);
-    V += __shfl(vi, 63);
+    uint2 w = make_uint2(0, 0);
+    if (on) __builtin_memcpy(&w, meta + e, 8);  // meta[e], meta[e + 1]
+    const uint32_t p = w.x & 0xffffu, kl = w.x >> 16, p1 = w.y & 0xffffu;
+    const uint32_t vl = on ? p1 - p - 10 - kl : 0u;
+    uint32_t ksum;
+    const uint32_t inc = wave_incl_add(kl, lane, ksum);
+    wave_lds_fence();  // every lane has read meta[e + 1] before it is rewritten
+    if (on) meta[e] = p | ((K + inc - kl) << 16);
+    K += ksum;
+    kmax = max(kmax, kl);
+    vmax = max(vmax, vl);
   }
-  if (lane == 0)
-    *reinterpret_cast<ushort4*>(meta + 4 * r.n) =
-        make_ushort4((uint16_t)r.end_pos, (uint16_t)K, 0, (uint16_t)V);
-  return WalkResult{r.n, K, V, r.status, r.base_pos, r.end_pos};
+  kmax = wave_max(kmax);
+  vmax = wave_max(vmax);
+  if (lane == 0) meta[r.n] = r.stop | (K << 16);
+  wave_lds_fence();
+  pl.n = r.n;
+  pl.K = K;
+  pl.V = r.stop - 10 * r.n - K;
+  auto jlog = [](uint32_t mx) -> uint32_t {  // lanes per entry: pieces of the longest entry
+    const uint32_t c = mx >= 16 ? (mx + 15) / 16 : 2u;
+    uint32_t j = 0;
+    while ((1u << j) < c && j < 6) j++;
+    return j;
+  };
+  pl.jk = jlog(kmax);
+  pl.jv = jlog(vmax);
 }
 
 struct Tot {
   uint32_t n, k, v;
 };
 
-constexpr uint32_t kMaxSpins = 1u << 20;  // ~1 s of polling: a hard bound, never expected
+constexpr uint32_t kMaxSpins = 1u << 16;  // ~4 ms of polling: a hard bound, never expected
 
 __device__ __forceinline__ void flag_timeout(uint64_t* result, uint32_t lane) {
   if (lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(result + 5), 2ull);
 }
 
-__device__ __forceinline__ uint32_t wave_sum_sat(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = sat_add(v, __shfl_xor(v, o));
+// Saturating (u32) wave scan / sum: DPP row_shr inside 16-lane rows, rows combined through
+// v_readlane (the prefix protocol's values saturate instead of wrapping).
+__device__ __forceinline__ uint32_t row_incl_sat(uint32_t v) {
+  v = sat_add(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true));
+  v = sat_add(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true));
+  v = sat_add(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true));
+  v = sat_add(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true));
   return v;
 }
 __device__ __forceinline__ uint32_t wave_scan_sat(uint32_t v, uint32_t lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t x = __shfl_up(v, o);
-    if (lane >= (uint32_t)o) v = sat_add(v, x);
-  }
-  return v;
+  v = row_incl_sat(v);
+  const uint32_t r0 = __builtin_amdgcn_readlane(v, 15);
+  const uint32_t r1 = sat_add(r0, __builtin_amdgcn_readlane(v, 31));
+  const uint32_t r2 = sat_add(r1, __builtin_amdgcn_readlane(v, 47));
+  const uint32_t row = lane >> 4;
+  return sat_add(v, row == 0 ? 0u : row == 1 ? r0 : row == 2 ? r1 : r2);
+}
+__device__ __forceinline__ uint32_t wave_sum_sat(uint32_t v) {  // uniform result
+  v = row_incl_sat(v);
+  return sat_add(sat_add(__builtin_amdgcn_readlane(v, 15), __builtin_amdgcn_readlane(v, 31)),
+                 sat_add(__builtin_amdgcn_readlane(v, 47), __builtin_amdgcn_readlane(v, 63)));
 }
 __device__ __forceinline__ bool read3(const uint64_t* r, uint64_t tag, uint32_t& a, uint32_t& b,
                                       uint32_t& c) {
@@ -286,61 +318,39 @@ __device__ Tot lookback(const uint64_t* rec, uint32_t g, uint64_t tag, uint32_t 
   return ex;
 }
 
-// Exclusive {entries, key bytes, value bytes} of every tile before `tile`, given this tile's
-// aggregate (already published).  Called by ONE wave of the tile's workgroup.
-__device__ Tot tile_prefix(const DecodeParams& p, uint32_t tile, uint32_t ntiles, uint64_t tag,
-                           uint32_t lane) {
-  const uint32_t g = tile >> 6;
+// A group = 64 consecutive blocks (all in one round of the persistent grid).  Every block
+// publishes its aggregate {entries, key bytes, value bytes} (lb[b][0..2], fire and forget);
+// one member per group and round -- rotating with the round, so no workgroup is always the
+// slow one -- collects the group's aggregates, scans them, looks back over earlier groups
+// and publishes every member's exclusive prefix (lb[b][4..6]).  No returning atomics.
+__device__ void group_lead(const DecodeParams& p, uint32_t b, uint64_t tag, uint32_t lane) {
+  const uint32_t g = b >> 6;
   const uint32_t g0 = g << 6;
-  const uint32_t gsize = (ntiles - g0 < 64u) ? (ntiles - g0) : 64u;
-  uint32_t old = 0;
-  if (lane == 0) old = atomicAdd(p.gcnt + g, 1u);
-  old = uniform(old);
-  if (old != gsize - 1) {
-    // a member: wait for the group's last arriver to publish this tile's exclusive prefix
-    const uint64_t* X = p.lb + (uint64_t)tile * 8 + 4;
-    for (uint32_t spins = 0;; ++spins) {
-      uint64_t x = 0;
-      bool ok = true;
-      if (lane < 3) {
-        x = gload(X + lane);
-        ok = (x >> kTagShift) == tag;
-      }
-      if (__all(ok)) {
-        const uint32_t v = (uint32_t)x;
-        return Tot{__shfl(v, 0), __shfl(v, 1), __shfl(v, 2)};
-      }
-      if (spins > kMaxSpins) {
-        flag_timeout(p.result, lane);
-        return Tot{0, 0, 0};
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  // the last arriver of group g: lane j reads tile g0+j's aggregate
-  uint32_t a = 0, b = 0, c = 0;
+  const uint32_t gsize = (p.nblk - g0 < 64u) ? (p.nblk - g0) : 64u;
+  uint32_t a = 0, bk = 0, c = 0;
   for (uint32_t spins = 0;; ++spins) {
     bool ok = true;
-    if (lane < gsize) ok = read3(p.lb + (uint64_t)(g0 + lane) * 8, tag, a, b, c);
+    if (lane < gsize) ok = read3(p.lb + (uint64_t)(g0 + lane) * 8, tag, a, bk, c);
     if (__all(ok)) break;
     if (spins > kMaxSpins) {
       flag_timeout(p.result, lane);
       break;
     }
-    __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_s_sleep(1);
   }
-  const uint32_t ia = wave_scan_sat(a, lane), ib = wave_scan_sat(b, lane),
+  const uint32_t ia = wave_scan_sat(a, lane), ib = wave_scan_sat(bk, lane),
                  ic = wave_scan_sat(c, lane);
-  uint64_t* G = p.glb + (uint64_t)g * 8;
+  const uint32_t ta = readlane(ia, gsize - 1), tb = readlane(ib, gsize - 1),
+                 tc = readlane(ic, gsize - 1);
+  uint64_t* Gr = p.glb + (uint64_t)g * 8;
   Tot pg{0, 0, 0};
   if (g > 0) {
-    store3(G, tag, __shfl(ia, gsize - 1), __shfl(ib, gsize - 1), __shfl(ic, gsize - 1), lane);
+    store3(Gr, tag, ta, tb, tc, lane);
     pg = lookback(p.glb, g, tag, lane, p.result);
   }
-  store3(G + 4, tag, sat_add(pg.n, __shfl(ia, gsize - 1)), sat_add(pg.k, __shfl(ib, gsize - 1)),
-         sat_add(pg.v, __shfl(ic, gsize - 1)), lane);
+  store3(Gr + 4, tag, sat_add(pg.n, ta), sat_add(pg.k, tb), sat_add(pg.v, tc), lane);
   // exclusive = group prefix + inclusive - own (own <= inclusive unless saturated)
-  const uint32_t ea = sat_add(pg.n, ia - a), eb = sat_add(pg.k, ib == 0xffffffffu ? ib : ib - b),
+  const uint32_t ea = sat_add(pg.n, ia - a), eb = sat_add(pg.k, ib == 0xffffffffu ? ib : ib - bk),
                  ec = sat_add(pg.v, ic - c);
   if (lane < gsize) {
     uint64_t* Xj = p.lb + (uint64_t)(g0 + lane) * 8 + 4;
@@ -348,176 +358,97 @@ __device__ Tot tile_prefix(const DecodeParams& p, uint32_t tile, uint32_t ntiles
     gstore(Xj + 1, (tag << kTagShift) | eb);
     gstore(Xj + 2, (tag << kTagShift) | ec);
   }
-  const uint32_t me = tile - g0;
-  return Tot{__shfl(ea, me), __shfl(eb, me), __shfl(ec, me)};
 }
 
-// Blend bytes [a, b) (0 <= a < b <= 16) of w into acc (v_bfi per dword).
-__device__ __forceinline__ uint32_t byte_mask(uint32_t a, uint32_t b, uint32_t d) {
-  const uint32_t lo = a > 4 * d ? (a - 4 * d > 4 ? 4 : a - 4 * d) : 0;
-  const uint32_t hi = b > 4 * d ? (b - 4 * d > 4 ? 4 : b - 4 * d) : 0;
-  return (uint32_t)((1ull << (8 * hi)) - 1) & ~(uint32_t)((1ull << (8 * lo)) - 1);
-}
-__device__ __forceinline__ void blend16(uint4& acc, const uint4& w, uint32_t a, uint32_t b) {
-  uint32_t m;
-  m = byte_mask(a, b, 0); acc.x = (acc.x & ~m) | (w.x & m);
-  m = byte_mask(a, b, 1); acc.y = (acc.y & ~m) | (w.y & m);
-  m = byte_mask(a, b, 2); acc.z = (acc.z & ~m) | (w.z & m);
-  m = byte_mask(a, b, 3); acc.w = (acc.w & ~m) | (w.w & m);
+// Block b's exclusive prefix from a granule poll issued earlier (lanes 0..2 hold x); polls
+// again until the group leader has published it.
+__device__ __forceinline__ Tot prefix_of(const DecodeParams& p, uint32_t b, uint64_t x,
+                                         uint64_t tag, uint32_t lane) {
+  const uint64_t* X = p.lb + (uint64_t)b * 8 + 4;
+  for (uint32_t spins = 0;; ++spins) {
+    const bool ok = lane >= 3 || (x >> kTagShift) == tag;
+    if (__all(ok)) {
+      const uint32_t v = (uint32_t)x;
+      return Tot{readlane(v, 0), readlane(v, 1), readlane(v, 2)};
+    }
+    if (spins > kMaxSpins) {
+      flag_timeout(p.result, lane);
+      return Tot{0, 0, 0};
+    }
+    __builtin_amdgcn_s_sleep(1);
+    if (lane < 3) x = gload(X + lane);
+  }
 }
 
-// Stream bytes [t, hi) of one block assembled into a 16-B register image whose byte i is
-// stream byte t0 + i, starting from entry e (o(e) <= t).  Stream byte t of entry e: values
-// -> block byte vs(e) + (t - vo(e)); keys -> u = t - ko(e) < plen(e) ? baseKey prefix
-// (block byte base_pos + u) : stored diff (ks(e) + u - plen(e)) -- blockIterator.parseKV,
-// iterator.go:98-100.  Each contiguous run is one unaligned 16-B LDS window + a byte blend.
+// ---------------------------------------------------------------------------------- emit
+// Entry e of one stream: output range [o, o1) comes from block bytes starting at s.
+// meta[e] = header pos | key offset << 16 (sentinel at n).
 template <bool IS_KEY>
-__device__ __forceinline__ uint4 assemble(const uint8_t* slot, uint32_t sh, const uint16_t* meta,
-                                          uint32_t e, uint32_t base_pos, int32_t t0, uint32_t t,
-                                          uint32_t hi) {
-  uint4 acc = make_uint4(0, 0, 0, 0);
-  ushort4 me = *reinterpret_cast<const ushort4*>(meta + 4 * e);
-  ushort4 mn = *reinterpret_cast<const ushort4*>(meta + 4 * e + 4);
-  while (t < hi) {
-    uint32_t o0 = IS_KEY ? me.y : me.w, o1 = IS_KEY ? mn.y : mn.w;
-    while (o1 <= t) {  // next entry (skips empty ones); never passes the sentinel since t < L
-      e++;
-      me = mn;
-      mn = *reinterpret_cast<const ushort4*>(meta + 4 * e + 4);
-      o0 = o1;
-      o1 = IS_KEY ? mn.y : mn.w;
-    }
-    const uint32_t u = t - o0;
-    uint32_t src, rend;
-    if (!IS_KEY) {
-      src = me.z + u;
-      rend = o1;
-    } else {
-      const uint32_t plen = (o1 - o0) - ((uint32_t)me.z - me.x);
-      if (u < plen) {
-        src = base_pos + u;
-        rend = o0 + plen;
-      } else {
-        src = me.x + (u - plen);
-        rend = o1;
-      }
-    }
-    if (rend > hi) rend = hi;
-    const uint32_t a = t - (uint32_t)t0;  // chunk byte of this run's start (0..15)
-    // window whose byte a is block byte src (>= 16 addressable LDS bytes precede the block)
-    const uint4 w = lds_u128(slot - 16, sh + src + 16 - a);
-    blend16(acc, w, a, rend - (uint32_t)t0);
-    t = rend;
+__device__ __forceinline__ void entry_span(const uint32_t* meta, uint32_t e, uint32_t& o,
+                                           uint32_t& o1, uint32_t& s) {
+  uint2 w;
+  __builtin_memcpy(&w, meta + e, 8);  // meta[e], meta[e + 1]: one ds_read_b64
+  const uint32_t p0 = w.x & 0xffffu, k0 = w.x >> 16, p1 = w.y & 0xffffu, k1 = w.y >> 16;
+  if (IS_KEY) {
+    o = k0;
+    o1 = k1;
+    s = p0 + 10;
+  } else {
+    o = p0 - 10 * e - k0;
+    o1 = p1 - 10 * (e + 1) - k1;
+    s = p0 + 10 + (k1 - k0);
   }
-  return acc;
 }
 
-__device__ __forceinline__ void store_bytes(uint8_t* dst, const uint4& v, uint32_t a, uint32_t b) {
-  const uint32_t words[4] = {v.x, v.y, v.z, v.w};
-  for (uint32_t i = a; i < b; i++) dst[i] = (uint8_t)(words[i >> 2] >> (8 * (i & 3)));
-}
-
-// Writes stream bytes [0, L) of one block to dst (global, any alignment): lane e owns every
-// aligned 16-B output chunk whose first byte lies inside entry e's output range -- interior
-// chunks are one LDS window and one dwordx4 store; a chunk that crosses into later entries is
-// assembled run by run.  Entry 0's lane also writes the stream's leading partial chunk, and
-// the chunk past the stream end is written byte-wise (the neighbouring block owns the rest).
+// One stream (keys or values) of one block.  Entry e's bytes [o, o1) are copied as pieces of
+// `sz` bytes (16, or 8/4/2/1 for entries shorter than 16): piece j covers entry bytes
+// [min(j*sz, len - sz), +sz) -- the last piece overlaps back inside the entry, so no store
+// ever touches a byte outside it (no read-modify-write, no cross-block ownership).  Loads
+// and stores are unaligned (one ds_read_b128 + one global_store_dwordx4 for a 16-B piece).
+// J = 2^jl lanes per entry; pieces beyond J are looped.
 template <bool IS_KEY>
-__device__ void emit_stream(uint8_t* dst, uint32_t L, const uint8_t* slot, uint32_t sh,
-                            const uint16_t* meta, uint32_t n, uint32_t base_pos, uint32_t lane) {
-  if (L == 0) return;
-  const uint32_t h = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);
-  uint8_t* dal = dst - h;  // chunk q covers stream bytes [16q - h, 16q - h + 16)
-  for (uint32_t e = lane; e < n; e += kWave) {
-    const ushort4 me = *reinterpret_cast<const ushort4*>(meta + 4 * e);
-    const ushort4 mn = *reinterpret_cast<const ushort4*>(meta + 4 * e + 4);
-    const uint32_t o0 = IS_KEY ? me.y : me.w, o1 = IS_KEY ? mn.y : mn.w;
-    if (e == 0 && h != 0) {  // leading partial chunk: stream bytes [0, min(16 - h, L))
-      const uint32_t hi = (16 - h < L) ? 16 - h : L;
-      const uint4 v = assemble<IS_KEY>(slot, sh, meta, 0, base_pos, -(int32_t)h, 0, hi);
-      store_bytes(dal, v, h, h + hi);
-    }
-    if (o0 == o1) continue;
-    const uint32_t plen = IS_KEY ? (o1 - o0) - ((uint32_t)me.z - me.x) : 0u;
-    for (uint32_t q = (o0 + h + 15) >> 4; 16 * q < o1 + h; q++) {
-      const int32_t t0 = (int32_t)(16 * q) - (int32_t)h;  // >= o0 >= 0
-      const uint32_t ut0 = (uint32_t)t0;
-      if (ut0 + 16 > L) {  // trailing partial chunk
-        const uint4 v = assemble<IS_KEY>(slot, sh, meta, e, base_pos, t0, ut0, L);
-        store_bytes(dal + 16 * q, v, 0, L - ut0);
-        continue;
-      }
-      uint4 v;
-      const uint32_t u0 = ut0 - o0;
-      if (ut0 + 16 <= o1 && (!IS_KEY || u0 >= plen)) {        // inside the value / key diff
-        v = lds_u128(slot, sh + (IS_KEY ? me.x + (u0 - plen) : me.z + u0));
-      } else if (IS_KEY && u0 + 16 <= plen) {                  // inside the baseKey prefix
-        v = lds_u128(slot, sh + base_pos + u0);
+__device__ __forceinline__ void emit_pieces(uint8_t* dst, const uint8_t* src, const uint32_t* meta,
+                                            uint32_t n, uint32_t jl, uint32_t lane) {
+  const uint32_t J = 1u << jl;
+  const uint32_t epi = kWave >> jl;  // entries per wave iteration
+  const uint32_t j0 = lane & (J - 1);
+  for (uint32_t e0 = 0; e0 < n; e0 += epi) {
+    const uint32_t e = e0 + (lane >> jl);
+    if (e >= n) continue;
+    uint32_t o, o1, s;
+    entry_span<IS_KEY>(meta, e, o, o1, s);
+    const uint32_t len = o1 - o;
+    const uint32_t sz = len >= 16 ? 16u : len >= 8 ? 8u : len >= 4 ? 4u : len >= 2 ? 2u : len;
+    const uint32_t np = len >= 16 ? (len + 15) >> 4 : (len > sz ? 2u : (len ? 1u : 0u));
+    for (uint32_t j = j0; j < np; j += J) {
+      const uint32_t off = min(j * sz, len - sz);
+      const uint8_t* sp = src + s + off;
+      uint8_t* dp = dst + o + off;
+      if (sz == 16) {
+        uint4 v;
+        __builtin_memcpy(&v, sp, 16);
+        __builtin_memcpy(dp, &v, 16);
+      } else if (sz == 8) {
+        uint2 v;
+        __builtin_memcpy(&v, sp, 8);
+        __builtin_memcpy(dp, &v, 8);
+      } else if (sz == 4) {
+        uint32_t v;
+        __builtin_memcpy(&v, sp, 4);
+        __builtin_memcpy(dp, &v, 4);
+      } else if (sz == 2) {
+        uint16_t v;
+        __builtin_memcpy(&v, sp, 2);
+        __builtin_memcpy(dp, &v, 2);
       } else {
-        v = assemble<IS_KEY>(slot, sh, meta, e, base_pos, t0, ut0, ut0 + 16);
+        *dp = *sp;
       }
-      *reinterpret_cast<uint4*>(dal + 16 * q) = v;
     }
-  }
-}
-
-// Bytes [lo, hi) of the 16-B chunk that starts at stream byte t0, for a stream whose entry e
-// occupies [o(e), o(e+1)) and comes from block bytes starting at src(e) (no prefixes: keys of
-// a plen == 0 block or values).  Entry e must contain lo.  One window + blend per entry run.
-template <int OCOL, int SCOL>
-__device__ __forceinline__ uint4 assemble_plain(const uint8_t* slot, uint32_t sh,
-                                                const uint16_t* meta, uint32_t e, int32_t t0,
-                                                uint32_t lo, uint32_t hi) {
-  uint4 acc = make_uint4(0, 0, 0, 0);
-  uint32_t t = lo;
-  uint32_t o0 = meta[4 * e + OCOL], s0 = meta[4 * e + SCOL];
-  while (t < hi) {
-    const uint32_t o1 = meta[4 * (e + 1) + OCOL];
-    const uint32_t rend = o1 < hi ? o1 : hi;
-    if (rend > t) {
-      const uint32_t a = t - (uint32_t)t0;
-      const uint4 w = lds_u128(slot - 16, sh + s0 + (t - o0) + 16 - a);
-      blend16(acc, w, a, rend - (uint32_t)t0);
-      t = rend;
-    }
-    e++;
-    o0 = o1;
-    s0 = meta[4 * e + SCOL];
-  }
-  return acc;
-}
-
-// One stream (OCOL = output-offset column, SCOL = block-position column) of one block,
-// lane-per-entry: interior chunks are one window + one aligned dwordx4 store; the chunk that
-// crosses the entry's end is assembled; the stream's partial head / tail chunks are stored
-// byte-wise (the neighbouring blocks own the other bytes of those chunks).
-template <int OCOL, int SCOL>
-__device__ __forceinline__ void emit_plain(uint8_t* dst, uint32_t L, const uint8_t* slot,
-                                           uint32_t sh, const uint16_t* meta, uint32_t e,
-                                           uint32_t o0, uint32_t o1, uint32_t s0, uint32_t h) {
-  uint8_t* dal = dst - h;  // chunk q covers stream bytes [16q - h, 16q - h + 16)
-  if (e == 0 && h != 0) {
-    const uint32_t hi = (16 - h < L) ? 16 - h : L;
-    const uint4 v = assemble_plain<OCOL, SCOL>(slot, sh, meta, 0, -(int32_t)h, 0, hi);
-    store_bytes(dal, v, h, h + hi);
-  }
-  // chunks fully inside [o0, o1)
-  const uint32_t qa = (o0 + h + 15) >> 4, qb = (o1 + h) >> 4;  // [qa, qb)
-  for (uint32_t q = qa; q < qb; q++)
-    *reinterpret_cast<uint4*>(dal + 16 * q) = lds_u128(slot, sh + s0 + (16 * q - h - o0));
-  // the chunk starting inside [o0, o1) that crosses o1 (or the stream end)
-  const uint32_t qc = qb > qa ? qb : qa;
-  const int32_t t0 = (int32_t)(16 * qc) - (int32_t)h;
-  if ((uint32_t)t0 < o1 && t0 >= (int32_t)o0) {
-    const uint32_t hi = ((uint32_t)t0 + 16 < L) ? (uint32_t)t0 + 16 : L;
-    const uint4 v = assemble_plain<OCOL, SCOL>(slot, sh, meta, e, t0, (uint32_t)t0, hi);
-    if (hi == (uint32_t)t0 + 16) *reinterpret_cast<uint4*>(dal + 16 * qc) = v;
-    else store_bytes(dal + 16 * qc, v, 0, hi - (uint32_t)t0);
   }
 }
 
 // Global-memory path with the same semantics: re-walks the block and copies every entry's
-// key and value with the wave's lanes (byte granular).  Used for oversize blocks only.
+// key and value with the wave's lanes (byte granular).  Oversize / prefix-compressed blocks.
 __device__ void emit_slow(const DecodeParams& p, const uint8_t* blk, uint32_t n, uint64_t ebase,
                           uint64_t kbase, uint64_t vbase, uint64_t off, uint32_t lane) {
   GlobalSrc src{blk};
@@ -549,43 +480,38 @@ __device__ void emit_slow(const DecodeParams& p, const uint8_t* blk, uint32_t n,
   }
 }
 
-// Workgroup rendezvous for LDS data only: unlike __syncthreads() it does not drain vmcnt,
-// so the next tile's prefetch loads and this tile's stream stores stay in flight.
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-template <int SLOT, int MAXE, int WPB>
-struct DecodeCfg {
-  static constexpr int kPad = 16;                  // addressable bytes before the block
-  static constexpr int kBuf = kPad + SLOT + 32;    // block (<= SLOT) at shift < 16 + over-read
-  static constexpr int kMeta = (MAXE + 1) * 8;
-  static constexpr int kWaveBytes = (2 * kBuf + kMeta + 15) & ~15;  // double-buffered slot
-  static constexpr int kShared = 64 + WPB * 16;    // tile base + per-wave aggregates
-  static constexpr int kLds = kWaveBytes * WPB + kShared;
-  static constexpr int kIters = (SLOT + 16 + 16 * kWave - 1) / (16 * kWave);  // 1-KiB DMA pieces
-};
-
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 
+// One LDS-DMA piece: lane l's 16 bytes at gptr -> LDS lds + 16 * l (global_load_lds_dwordx4,
+// M0 = LDS base).  Inline asm ON PURPOSE: the compiler treats an LDS-DMA it can see as a
+// writer of every LDS byte and drains vmcnt before the next LDS read -- which would make
+// each walk wait for the NEXT block's prefetch.  The kernel's own `s_waitcnt vmcnt(0)` at the
+// top of each iteration is what orders a block's DMA before its reads.
+__device__ __forceinline__ void dma16(const uint8_t* gptr, uint8_t* lds) {
+  const uint32_t m0 = uniform((uint32_t)(uintptr_t)(lds_void_t*)lds);
+  uint32_t saved;  // M0 is reserved to the compiler: restore it
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(saved)
+      : "v"(gptr), "s"(m0)
+      : "memory");
+}
+
 struct BlockRef {
-  uint64_t off;
-  uint32_t len, sh;
+  uint32_t off, len, sh;
   bool fits, tail;  // tail: a chunk crosses the end of the data buffer (loaded by lanes)
 };
 
-// Issue block b's bytes into `buf` by LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave
-// instruction, no VGPRs), 16-B aligned source; the chunk crossing the end of the data buffer
-// (last block only) is left for land_tail().
+// Block [off, off + len): if it fits the slot, its bytes are issued into `buf` by LDS-DMA
+// (global_load_lds_dwordx4: 1 KiB per wave instruction, no VGPRs), 16-B aligned source; the
+// chunk crossing the end of the data buffer (last block only) is left for land_tail().
 template <int SLOT, int ITERS>
-__device__ __forceinline__ BlockRef prefetch_block(const DecodeParams& p, uint32_t b, uint8_t* buf,
-                                                   uint32_t lane) {
-  BlockRef r{0, 0, 0, false, false};
-  if (b >= p.nblk) return r;
-  r.off = uniform(p.blk_off[b]);
-  r.len = uniform(p.blk_len[b]);
-  r.fits = r.len <= (uint32_t)SLOT && r.off + r.len <= p.data_len;
+__device__ __forceinline__ BlockRef prefetch_block(const DecodeParams& p, uint32_t off,
+                                                   uint32_t len, uint8_t* buf, uint32_t lane) {
+  BlockRef r{off, len, 0, false, false};
+  r.fits = r.len <= (uint32_t)SLOT && (uint64_t)r.off + r.len <= p.data_len;
   if (!r.fits) return r;
   const uint64_t a0 = r.off & ~15ull;
   r.sh = (uint32_t)(r.off - a0);
@@ -595,9 +521,7 @@ __device__ __forceinline__ BlockRef prefetch_block(const DecodeParams& p, uint32
   for (int i = 0; i < ITERS; i++) {
     const uint32_t c = lane + i * kWave;
     const uint64_t a = a0 + 16ull * c;
-    if (c < nchunk && a + 16 <= p.data_len)
-      __builtin_amdgcn_global_load_lds((glb_void_t*)(p.data + a), (lds_void_t*)(buf + i * 1024),
-                                       16, 0, 0);
+    if (c < nchunk && a + 16 <= p.data_len) dma16(p.data + a, buf + i * 1024);
   }
   return r;
 }
@@ -615,215 +539,641 @@ __device__ __forceinline__ void land_tail(const DecodeParams& p, const BlockRef&
   }
 }
 
-template <int SLOT, int MAXE, int WPB>
-__global__ void __launch_bounds__(WPB * 64) decode_kernel(DecodeParams p) {
-  using Cfg = DecodeCfg<SLOT, MAXE, WPB>;
+// Walk one block (its bytes already in `slot` when it fits): the emit plan + meta.
+template <int SLOT, int MAXE>
+__device__ __forceinline__ Plan walk_stage(const DecodeParams& p, const BlockRef& ref, bool valid,
+                                           uint8_t* slot, uint32_t* meta, uint32_t lane,
+                                           uint64_t* spec_acc = nullptr) {
+  Plan pl{};
+  if (!valid) return pl;
+  pl.off = ref.off;
+  pl.len = ref.len;
+  pl.sh = ref.sh;
+  if ((uint64_t)ref.off + ref.len > p.data_len) {
+    pl.status = LSMGPU_BLK_RANGE;
+    return pl;
+  }
+  if (p.ablate & 4) return pl;
+  if (ref.fits) {
+    if (ref.tail) land_tail(p, ref, slot, lane);
+    wave_lds_fence();
+#ifdef LSMGPU_STAMPS
+    const uint64_t t0 = spec_acc ? __builtin_amdgcn_s_memtime() : 0;
+#endif
+    const SpecResult r = walk_spec(slot, ref.sh, ref.len, meta, MAXE, lane);
+#ifdef LSMGPU_STAMPS
+    if (spec_acc) {
+      spec_acc[0] += __builtin_amdgcn_s_memtime() - t0;
+      spec_acc[1] += r.rounds;
+    }
+#endif
+    pl.status = r.status;
+    if (r.n <= (uint32_t)MAXE && !r.any_plen) {
+      finish_meta(meta, r, lane, pl);
+      pl.kind = pl.n ? 1u : 0u;
+      return pl;
+    }
+  }
+  const WalkResult w = walk_block(GlobalSrc{p.data + ref.off}, ref.len);
+  pl.n = w.n;
+  pl.K = w.K;
+  pl.V = w.V;
+  pl.status = w.status;
+  pl.kind = w.n ? 2u : 0u;
+  return pl;
+}
+
+// Write one block's outputs at its global bases.
+__device__ __forceinline__ void emit_block(const DecodeParams& p, const Plan& pl, uint32_t b,
+                                           Tot ex, const uint8_t* slot, const uint32_t* meta,
+                                           uint32_t lane) {
+  if (lane == 0) {
+    if (p.blk_first) p.blk_first[b] = ex.n;
+    if (p.blk_status) p.blk_status[b] = (int32_t)pl.status;
+    if (pl.status != LSMGPU_BLK_OK) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(p.result + 4), 1ull);
+      atomicMax(reinterpret_cast<unsigned long long*>(p.result + 3),
+                (unsigned long long)(p.nblk - b));
+    }
+  }
+  const bool mat = (p.mode & LSMGPU_MODE_MATERIALIZE) != 0;
+  const bool view = (p.mode & LSMGPU_MODE_VIEW) != 0 && p.view;
+  bool ok = (uint64_t)ex.n + pl.n <= p.ent_cap;
+  if (mat) {
+    const uint64_t kend = (uint64_t)ex.k + pl.K, vend = (uint64_t)ex.v + pl.V;
+    ok = ok && (kend <= p.key_cap || !p.key_data) && (vend <= p.val_cap || !p.val_data);
+    ok = ok && kend < 0xffffffffull && vend <= 0xffffffffull;
+  }
+  if (!ok && lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(p.result + 5), 1ull);
+  if (!ok || pl.kind == 0 || (p.ablate & 2)) return;
+  if (pl.kind == 2) {
+    emit_slow(p, p.data + pl.off, pl.n, ex.n, ex.k, ex.v, pl.off, lane);
+    return;
+  }
+  // per-entry end offsets / view records (lane per entry)
+  for (uint32_t e = lane; e < pl.n; e += kWave) {
+    const uint32_t w0 = meta[e], w1 = meta[e + 1];
+    const uint32_t p0 = w0 & 0xffffu, k0 = w0 >> 16, p1 = w1 & 0xffffu, k1 = w1 >> 16;
+    const uint32_t vo1 = p1 - 10 * (e + 1) - k1;
+    if (mat) {
+      if (p.key_end) p.key_end[ex.n + e] = ex.k + k1;
+      if (p.val_end) p.val_end[ex.n + e] = ex.v + vo1;
+    }
+    if (view) {
+      const uint32_t klen = k1 - k0, vlen = vo1 - (p0 - 10 * e - k0);
+      p.view[ex.n + e] = (uint64_t)(pl.off + p0 + 10) | ((uint64_t)klen << 32) |
+                         ((uint64_t)vlen << 48);
+    }
+  }
+  if (!mat) return;
+  const uint8_t* src = slot + pl.sh;  // block byte 0
+  if (p.key_data) emit_pieces<true>(p.key_data + ex.k, src, meta, pl.n, pl.jk, lane);
+  if (p.val_data) emit_pieces<false>(p.val_data + ex.v, src, meta, pl.n, pl.jv, lane);
+}
+
+// The walk's plan of a block, parked in LDS next to its metadata until the block is emitted
+// (two iterations later).
+constexpr int kPlanWords = 10;
+__device__ __forceinline__ void plan_store(uint32_t* rec, const Plan& pl, uint32_t lane) {
+  const uint32_t v[kPlanWords] = {pl.n, pl.K, pl.V, pl.status, pl.off, pl.len, pl.sh, pl.kind, pl.jk, pl.jv};
+  if (lane < (uint32_t)kPlanWords) {
+    uint32_t x = v[0];
+#pragma unroll
+    for (int i = 1; i < kPlanWords; i++) x = lane == (uint32_t)i ? v[i] : x;
+    rec[lane] = x;
+  }
+}
+__device__ __forceinline__ Plan plan_load(const uint32_t* rec) {
+  Plan pl;
+  pl.n = uniform(rec[0]);
+  pl.K = uniform(rec[1]);
+  pl.V = uniform(rec[2]);
+  pl.status = uniform(rec[3]);
+  pl.off = uniform(rec[4]);
+  pl.len = uniform(rec[5]);
+  pl.sh = uniform(rec[6]);
+  pl.kind = uniform(rec[7]);
+  pl.jk = uniform(rec[8]);
+  pl.jv = uniform(rec[9]);
+  return pl;
+}
+
+template <int SLOT, int MAXE, int NS>
+struct DecodeCfg {
+  static_assert(NS >= 3, "the emit lags the walk by NS - 2 >= 1 blocks");
+  static constexpr int kLag = NS - 2;
+  static constexpr int kBuf = SLOT + 16;                  // block at shift < 16, 16-B DMA pieces
+  static constexpr int kNM = NS - 1;                      // metadata of blocks k-kLag .. k
+  static constexpr int kMetaWords = MAXE + 2 + kPlanWords + 2;  // {pos|koff<<16}[n+1], plan
+  static constexpr int kLds = NS * kBuf + kNM * kMetaWords * 4;
+  static constexpr int kIters = (SLOT + 16 + 16 * kWave - 1) / (16 * kWave);  // 1-KiB DMA pieces
+};
+
+// Residency census: every workgroup arrives and waits (bounded, 2 ms) for the whole grid.
+__device__ void census(uint32_t* c, uint32_t lane) {
+  if (lane != 0) return;
+  atomicAdd(c, 1u);
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+  while (__builtin_amdgcn_s_memrealtime() - t0 < 200000ull) {
+    if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= gridDim.x) {
+      atomicAdd(c + 1, 1u);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+
+__device__ __forceinline__ uint64_t stamp() { return __builtin_amdgcn_s_memtime(); }
+
+// One wave per workgroup; workgroup w decodes blocks w, w + G, w + 2G, ... (G = grid size, a
+// multiple of 64, fully resident).  Iteration k (one vmcnt drain per iteration):
+//   a. s_waitcnt vmcnt(0): block k's LDS-DMA, block k-L's prefix poll and block k-L-1's
+//      stores, all issued one iteration (a whole walk) ago
+//   b. emit block k-L (its base from the poll; L = NS - 2 = 2 blocks behind the walk)
+//   c. issue block k+1's LDS-DMA (into block k-L-1's slot) and block k-L+1's prefix poll
+//   d. walk block k from LDS, park its plan, publish its aggregate; the round's group leader
+//      publishes its group's prefixes
+template <int SLOT, int MAXE, int NS>
+__global__ void __launch_bounds__(64) decode_kernel(DecodeParams p) {
+  using Cfg = DecodeCfg<SLOT, MAXE, NS>;
+  constexpr uint32_t L = Cfg::kLag;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = lane_id();
-  const uint32_t wv = uniform(threadIdx.x >> 6);
-  uint8_t* wbase = smem + wv * Cfg::kWaveBytes;
-  uint16_t* meta = reinterpret_cast<uint16_t*>(wbase + 2 * Cfg::kBuf);
-  uint32_t* s_base = reinterpret_cast<uint32_t*>(smem + WPB * Cfg::kWaveBytes);  // [3]
-  uint32_t* s_agg = s_base + 16;                                                // [WPB][4]
+  if (p.census) {
+    census(p.census, lane);
+    return;
+  }
+  const uint32_t G = gridDim.x, w = blockIdx.x, nblk = p.nblk;
   const uint64_t tag = p.tag;
-  const uint32_t ntiles = (p.nblk + WPB - 1) / WPB;
+  const uint32_t K = w < nblk ? (nblk - 1 - w) / G + 1 : 0;  // this workgroup's blocks
+  uint32_t* meta_base = reinterpret_cast<uint32_t*>(smem + NS * Cfg::kBuf);
+  auto slot_of = [&](uint32_t k) -> uint8_t* { return smem + (k % NS) * Cfg::kBuf; };
+  auto meta_of = [&](uint32_t k) -> uint32_t* { return meta_base + (k % Cfg::kNM) * Cfg::kMetaWords; };
+  auto blk_of = [&](uint32_t k) -> uint32_t { return w + k * G; };
+  // lane i holds [off, len) of block k0 + i of this workgroup: 64 iterations per load
+  uint32_t ring_k0 = 0, ring_off = 0, ring_len = 0;
+  auto ring_load = [&](uint32_t k0) {
+    ring_k0 = k0;
+    const uint64_t b = (uint64_t)w + (uint64_t)(k0 + lane) * G;
+    ring_off = b < nblk ? p.blk_off[b] : 0u;
+    ring_len = b < nblk ? p.blk_len[b] : 0u;
+  };
+#ifdef LSMGPU_STAMPS
+  // diagnostic build only (LSMGPU_BUILD_STAMPS=1): per-phase s_memtime totals
+  const bool st = p.stamps != nullptr;
+  uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tprev = st ? stamp() : 0;
+  auto mark = [&](int i) {
+    if (st) {
+      const uint64_t t = stamp();
+      acc[i] += t - tprev;
+      tprev = t;
+    }
+  };
+  uint64_t* spec_acc = st ? &acc[6] : nullptr;
+#else
+  auto mark = [](int) {};
+  uint64_t* spec_acc = nullptr;
+#endif
 
-  // Static round-robin over a fully resident grid (gridDim.x a multiple of 64 workgroups, or
-  // >= the tile count): a 64-tile group lies inside one round, every wait points at an
-  // earlier group or at a member of the same group in the same round -> no deadlock; spins
-  // are bounded anyway.  (A shared ticket counter would serialise at ~88 atomics/us.)
-  uint32_t tile = blockIdx.x;
-  uint32_t cur = 0;
-  BlockRef ref = prefetch_block<SLOT, Cfg::kIters>(p, tile * WPB + wv, wbase + Cfg::kPad, lane);
-  for (; tile < ntiles; tile += gridDim.x) {
-    uint8_t* slot = wbase + cur * Cfg::kBuf + Cfg::kPad;
-    const uint32_t b = tile * WPB + wv;
-    const bool valid = b < p.nblk;
-    WalkResult w{0, 0, 0, LSMGPU_BLK_OK, 0, 0};
-    bool fast = false, any_plen = false;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's DMA has landed
-    if (valid) {
-      if (ref.off + ref.len > p.data_len) {
-        w.status = LSMGPU_BLK_RANGE;
-      } else if (ref.fits) {
-        if (ref.tail) land_tail(p, ref, slot, lane);
-        wave_lds_fence();
-        if (p.ablate & 4) {
-          w = WalkResult{0, 0, 0, 0, 0, 0};
-        } else {
-          const SpecResult r = walk_spec(slot, ref.sh, ref.len, meta, MAXE, lane);
-          if (r.n <= (uint32_t)MAXE) {
-            wave_lds_fence();
-            w = finish_meta(slot, ref.sh, r, meta, lane, any_plen);
-            fast = (w.K <= 0xffffu) && (w.V <= 0xffffu);
-          } else {  // too many entries for the metadata: count on the global path
-            w = walk_block(GlobalSrc{p.data + ref.off}, ref.len, meta, 0, false, lane);
-          }
-        }
-      } else {
-        w = walk_block(GlobalSrc{p.data + ref.off}, ref.len, meta, 0, false, lane);
-      }
-    }
-    // ---- tile scan of the per-block aggregates (LDS)
-    if (lane == 0) {
-      s_agg[4 * wv + 0] = w.n;
-      s_agg[4 * wv + 1] = w.K;
-      s_agg[4 * wv + 2] = w.V;
-    }
-    lds_barrier();
-    // next tile's block -> the other buffer, now: the DMA overlaps the prefix wait and the emit
-    const uint32_t next = tile + gridDim.x;
-    const BlockRef nref = prefetch_block<SLOT, Cfg::kIters>(
-        p, next * WPB + wv, wbase + (cur ^ 1) * Cfg::kBuf + Cfg::kPad, lane);
-    if (wv == 0) {
-      uint32_t a = 0, bk = 0, c = 0;
-      if (lane < (uint32_t)WPB) {
-        a = s_agg[4 * lane];
-        bk = s_agg[4 * lane + 1];
-        c = s_agg[4 * lane + 2];
-      }
-      const uint32_t ia = wave_scan_sat(a, lane), ib = wave_scan_sat(bk, lane),
-                     ic = wave_scan_sat(c, lane);
-      const uint32_t ta = __shfl(ia, WPB - 1), tb = __shfl(ib, WPB - 1), tc = __shfl(ic, WPB - 1);
+  BlockRef ref_next{0, 0, 0, false, false};
+  if (K > 0) {
+    ring_load(0);
+    ref_next = prefetch_block<SLOT, Cfg::kIters>(p, readlane(ring_off, 0), readlane(ring_len, 0),
+                                                 slot_of(0), lane);
+  }
+  uint64_t poll = 0;
+  for (uint32_t k = 0; k < K + L; k++) {
+    // a. one drain for everything issued an iteration ago
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const BlockRef ref = ref_next;
+    mark(0);
+    // b. emit block k - L
+    if (k >= L) {
+      const uint32_t ke = k - L, be = blk_of(ke);
       Tot ex{0, 0, 0};
+      if (!(p.ablate & 1)) ex = prefix_of(p, be, poll, tag, lane);
+      mark(5);
+      const uint32_t* rec = meta_of(ke);
+      const Plan pl = plan_load(rec + MAXE + 2);
+      if (be == nblk - 1 && lane == 0) {  // totals of the whole batch
+        if (p.blk_first) p.blk_first[nblk] = ex.n + pl.n;
+        p.result[0] = sat_add(ex.n, pl.n);
+        p.result[1] = sat_add(ex.k, pl.K);
+        p.result[2] = sat_add(ex.v, pl.V);
+      }
+      emit_block(p, pl, be, ex, slot_of(ke), rec, lane);
+    }
+    mark(1);
+    // c. next block's bytes, the next emit's prefix poll
+    if (k + 1 < K) {
+      if (k + 1 - ring_k0 >= (uint32_t)kWave) ring_load(k + 1);
+      const uint32_t i = k + 1 - ring_k0;
+      ref_next = prefetch_block<SLOT, Cfg::kIters>(p, readlane(ring_off, i), readlane(ring_len, i),
+                                                   slot_of(k + 1), lane);
+    }
+    if (k + 1 >= L && k + 1 - L < K && lane < 3 && !(p.ablate & 1))
+      poll = gload(p.lb + (uint64_t)blk_of(k + 1 - L) * 8 + 4 + lane);
+    mark(2);
+    // d. walk block k
+    if (k < K) {
+      const uint32_t b = blk_of(k);
+      uint32_t* rec = meta_of(k);
+      wave_lds_fence();
+      const Plan pl = walk_stage<SLOT, MAXE>(p, ref, true, slot_of(k), rec, lane, spec_acc);
+      plan_store(rec + MAXE + 2, pl, lane);
+      mark(3);
       if (!(p.ablate & 1)) {
-        store3(p.lb + (uint64_t)tile * 8, tag, ta, tb, tc, lane);
-        ex = tile_prefix(p, tile, ntiles, tag, lane);
+        store3(p.lb + (uint64_t)b * 8, tag, pl.n, pl.K, pl.V, lane);
+        const uint32_t g0 = b & ~63u;
+        const uint32_t gsize = (nblk - g0 < 64u) ? (nblk - g0) : 64u;
+        if ((b - g0) == (b / G) % gsize) group_lead(p, b, tag, lane);
       }
-      if (lane < (uint32_t)WPB) {  // per-block exclusive bases within the tile
-        s_agg[4 * lane] = ia - a;
-        s_agg[4 * lane + 1] = ib == 0xffffffffu ? ib : ib - bk;
-        s_agg[4 * lane + 2] = ic - c;
-      }
-      if (lane == 0) {
-        s_base[0] = ex.n;
-        s_base[1] = ex.k;
-        s_base[2] = ex.v;
-        if (tile == ntiles - 1) {
-          if (p.blk_first) p.blk_first[p.nblk] = ex.n + ta;
-          p.result[0] = sat_add(ex.n, ta);
-          p.result[1] = sat_add(ex.k, tb);
-          p.result[2] = sat_add(ex.v, tc);
-        }
-      }
+      mark(4);
     }
-    lds_barrier();
-    if (valid) {
-      const Tot ex{s_base[0] + s_agg[4 * wv], sat_add(s_base[1], s_agg[4 * wv + 1]),
-                   s_base[2] + s_agg[4 * wv + 2]};
-      if (lane == 0) {
-        if (p.blk_first) p.blk_first[b] = (uint32_t)ex.n;
-        if (p.blk_status) p.blk_status[b] = (int32_t)w.status;
-        if (w.status != LSMGPU_BLK_OK) {
-          atomicAdd(reinterpret_cast<unsigned long long*>(p.result + 4), 1ull);
-          atomicMax(reinterpret_cast<unsigned long long*>(p.result + 3),
-                    (unsigned long long)(p.nblk - b));
-        }
-      }
-      const bool mat = (p.mode & LSMGPU_MODE_MATERIALIZE) != 0;
-      const bool view = (p.mode & LSMGPU_MODE_VIEW) != 0 && p.view;
-      bool ok = (uint64_t)ex.n + w.n <= p.ent_cap;
-      if (mat) {
-        const uint64_t kend = (uint64_t)ex.k + w.K, vend = (uint64_t)ex.v + w.V;
-        ok = ok && (kend <= p.key_cap || !p.key_data) && (vend <= p.val_cap || !p.val_data);
-        ok = ok && kend < 0xffffffffull && vend <= 0xffffffffull;
-      }
-      if (!ok && lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(p.result + 5), 1ull);
-      if (ok && w.n > 0 && !(p.ablate & 2)) {
-        if (!fast) {
-          emit_slow(p, p.data + ref.off, w.n, ex.n, ex.k, ex.v, ref.off, lane);
-        } else {
-          const uint32_t en = ex.n, ek = ex.k, evv = ex.v;
-          const bool keys_plain = !any_plen;
-          const uint32_t hk = (uint32_t)(reinterpret_cast<uintptr_t>(p.key_data + ek) & 15u);
-          const uint32_t hv = (uint32_t)(reinterpret_cast<uintptr_t>(p.val_data + evv) & 15u);
-          // lane e: entry e's offsets / view record and the stream chunks starting inside it
-          for (uint32_t e = lane; e < w.n; e += kWave) {
-            const ushort4 me = *reinterpret_cast<const ushort4*>(meta + 4 * e);
-            const ushort4 mn = *reinterpret_cast<const ushort4*>(meta + 4 * e + 4);
-            if (mat) {
-              if (p.key_end) p.key_end[en + e] = ek + mn.y;
-              if (p.val_end) p.val_end[en + e] = evv + mn.w;
-              if (p.val_data)
-                emit_plain<3, 2>(p.val_data + evv, w.V, slot, ref.sh, meta, e, me.w, mn.w, me.z, hv);
-              if (p.key_data && keys_plain)
-                emit_plain<1, 0>(p.key_data + ek, w.K, slot, ref.sh, meta, e, me.y, mn.y, me.x, hk);
-            }
-            if (view) {
-              const uint32_t klen = (uint32_t)me.z - me.x, vlen = (uint32_t)mn.w - me.w;
-              p.view[en + e] = (uint64_t)(uint32_t)(ref.off + me.x) | ((uint64_t)klen << 32) |
-                               ((uint64_t)vlen << 48);
-            }
-          }
-          if (mat && p.key_data && !keys_plain)  // prefix-compressed keys (plen > 0)
-            emit_stream<true>(p.key_data + ek, w.K, slot, ref.sh, meta, w.n, w.base_pos, lane);
-        }
-      }
-    }
-    ref = nref;
-    cur ^= 1;
     wave_lds_fence();
   }
+#ifdef LSMGPU_STAMPS
+  if (st && lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) atomicAdd(reinterpret_cast<unsigned long long*>(p.stamps + i), acc[i]);
+    atomicAdd(reinterpret_cast<unsigned long long*>(p.stamps + 8), (unsigned long long)(K + L));
+    atomicAdd(reinterpret_cast<unsigned long long*>(p.stamps + 9), 1ull);
+  }
+#endif
+}
+
+// ====================================================================== 4 KiB blocks
+// Register-lag variant (blocks <= 4 KiB: the BASELINE C2 shape).  After block k is walked
+// its key and value streams are compacted into an LDS staging buffer (overlapping unaligned
+// pieces) and read back as <= 5 16-B chunks per lane: the block's OUTPUT then waits for its
+// prefix in VGPRs, not in LDS, so the emit can lag the walk by L = 3 blocks with only two
+// block slots + one staging buffer of LDS per wave (~12.9 KB -> 12 waves/CU).  The emit is
+// then <= 5 contiguous global_store_dwordx4 (the stream's last chunk overlaps back inside it)
+// plus the per-entry end offsets, with no LDS traffic.
+constexpr int kRegChunks = 5;  // 320 chunks per block >= (4096 + 16 + 16) / 16
+struct Pend {
+  uint4 c[kRegChunks];          // chunk q = 64 s + lane of [key stream | value stream]
+  uint32_t m0, m0n, m1, m1n;    // meta words of entries lane, lane + 1, 64 + lane, 65 + lane
+  uint32_t sc;                  // lane i = field i: n, K, V, status, off, len, kind
+};
+
+template <int MAXE>
+struct RegCfg {
+  static_assert(MAXE >= 128, "entry meta words for 128 entries are held in registers");
+  static constexpr int kSlot = 4096;
+  static constexpr int kBuf = kSlot + 16;
+  static constexpr int kStage = kSlot + 32;
+  static constexpr int kMetaWords = MAXE + 2;
+  static constexpr int kLds = 2 * kBuf + kStage + kMetaWords * 4;
+  static constexpr int kIters = (kSlot + 16 + 16 * kWave - 1) / (16 * kWave);
+};
+
+__device__ __forceinline__ uint32_t chunk_off(uint32_t q, uint32_t Q, uint32_t L) {
+  return q + 1 == Q ? L - 16 : 16 * q;  // the last chunk overlaps back inside the stream
+}
+
+// Walk + stage block k: fills `pd` (registers) from the block in `slot`.
+template <int MAXE>
+__device__ __forceinline__ void stage_block(const DecodeParams& p, const BlockRef& ref,
+                                            uint8_t* slot, uint8_t* stage, uint32_t* meta,
+                                            Pend& pd, uint32_t lane, uint64_t* spec_acc) {
+  Plan pl = walk_stage<4096, MAXE>(p, ref, true, slot, meta, lane, spec_acc);
+  if (pl.kind == 1 && (pl.n > 128 || pl.K < 16 || pl.V < 16)) pl.kind = 2;  // n, K, V exact
+  const uint32_t f[7] = {pl.n, pl.K, pl.V, pl.status, pl.off, pl.len, pl.kind};
+  uint32_t x = f[0];
+#pragma unroll
+  for (int i = 1; i < 7; i++) x = lane == (uint32_t)i ? f[i] : x;
+  pd.sc = x;
+  if (pl.kind != 1) return;
+  const uint8_t* src = slot + pl.sh;
+  emit_pieces<true>(stage, src, meta, pl.n, pl.jk, lane);
+  emit_pieces<false>(stage + pl.K, src, meta, pl.n, pl.jv, lane);
+  wave_lds_fence();
+  const uint32_t Qk = (pl.K + 15) >> 4, Qv = (pl.V + 15) >> 4;
+#pragma unroll
+  for (int s = 0; s < kRegChunks; s++) {
+    const uint32_t q = 64 * s + lane;
+    uint32_t o = 0;
+    if (q < Qk) o = chunk_off(q, Qk, pl.K);
+    else if (q < Qk + Qv) o = pl.K + chunk_off(q - Qk, Qv, pl.V);
+    uint4 v;
+    __builtin_memcpy(&v, stage + o, 16);
+    pd.c[s] = v;
+  }
+  uint2 w0, w1;
+  __builtin_memcpy(&w0, meta + lane, 8);
+  __builtin_memcpy(&w1, meta + 64 + lane, 8);
+  pd.m0 = w0.x;
+  pd.m0n = w0.y;
+  pd.m1 = w1.x;
+  pd.m1n = w1.y;
+}
+
+// Per-entry end offsets / view record of entry e from its meta words (this, next).
+__device__ __forceinline__ void entry_out(const DecodeParams& p, uint32_t e, uint32_t wm,
+                                          uint32_t wn, Tot ex, uint32_t off, bool mat, bool view) {
+  const uint32_t p0 = wm & 0xffffu, k0 = wm >> 16, p1 = wn & 0xffffu, k1 = wn >> 16;
+  const uint32_t vo1 = p1 - 10 * (e + 1) - k1;
+  if (mat) {
+    if (p.key_end) p.key_end[ex.n + e] = ex.k + k1;
+    if (p.val_end) p.val_end[ex.n + e] = ex.v + vo1;
+  }
+  if (view) {
+    const uint32_t klen = k1 - k0, vlen = vo1 - (p0 - 10 * e - k0);
+    p.view[ex.n + e] = (uint64_t)(off + p0 + 10) | ((uint64_t)klen << 32) | ((uint64_t)vlen << 48);
+  }
+}
+
+__device__ __forceinline__ void emit_pend(const DecodeParams& p, const Pend& pd, uint32_t b, Tot ex,
+                                          uint32_t lane) {
+  const uint32_t n = readlane(pd.sc, 0), K = readlane(pd.sc, 1), V = readlane(pd.sc, 2),
+                 status = readlane(pd.sc, 3), off = readlane(pd.sc, 4), kind = readlane(pd.sc, 6);
+  if (lane == 0) {
+    if (p.blk_first) p.blk_first[b] = ex.n;
+    if (p.blk_status) p.blk_status[b] = (int32_t)status;
+    if (status != LSMGPU_BLK_OK) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(p.result + 4), 1ull);
+      atomicMax(reinterpret_cast<unsigned long long*>(p.result + 3),
+                (unsigned long long)(p.nblk - b));
+    }
+  }
+  const bool mat = (p.mode & LSMGPU_MODE_MATERIALIZE) != 0;
+  const bool view = (p.mode & LSMGPU_MODE_VIEW) != 0 && p.view;
+  bool ok = (uint64_t)ex.n + n <= p.ent_cap;
+  if (mat) {
+    const uint64_t kend = (uint64_t)ex.k + K, vend = (uint64_t)ex.v + V;
+    ok = ok && (kend <= p.key_cap || !p.key_data) && (vend <= p.val_cap || !p.val_data);
+    ok = ok && kend < 0xffffffffull && vend <= 0xffffffffull;
+  }
+  if (!ok && lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(p.result + 5), 1ull);
+  if (!ok || kind == 0 || (p.ablate & 2)) return;
+  if (kind == 2) {
+    emit_slow(p, p.data + off, n, ex.n, ex.k, ex.v, off, lane);
+    return;
+  }
+  if (lane < n) entry_out(p, lane, pd.m0, pd.m0n, ex, off, mat, view);
+  if (64 + lane < n) entry_out(p, 64 + lane, pd.m1, pd.m1n, ex, off, mat, view);
+  if (!mat) return;
+  const uint32_t Qk = (K + 15) >> 4, Qv = (V + 15) >> 4;
+  uint8_t* kd = p.key_data + ex.k;
+  uint8_t* vd = p.val_data + ex.v;
+#pragma unroll
+  for (int s = 0; s < kRegChunks; s++) {
+    const uint32_t q = 64 * s + lane;
+    const uint4 v = pd.c[s];
+    if (q < Qk) {
+      if (p.key_data) __builtin_memcpy(kd + chunk_off(q, Qk, K), &v, 16);
+    } else if (q < Qk + Qv) {
+      if (p.val_data) __builtin_memcpy(vd + chunk_off(q - Qk, Qv, V), &v, 16);
+    }
+  }
+}
+
+// One wave per workgroup, blocks w, w + G, ...  Iteration k (one vmcnt drain):
+//   a. s_waitcnt vmcnt(0): block k's LDS-DMA, block k-L's prefix poll, old stores
+//   b. emit block k-L from registers (its base from the poll)
+//   c. issue block k+1-L's prefix poll and block k+1's LDS-DMA (the slot of block k-1)
+//   d. walk + stage block k into registers, publish its aggregate, lead its group if due
+template <int MAXE, int L>
+__global__ void __launch_bounds__(64) decode_reg_kernel(DecodeParams p) {
+  static_assert(L == 3, "three named pending slots");
+  using Cfg = RegCfg<MAXE>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t lane = lane_id();
+  if (p.census) {
+    census(p.census, lane);
+    return;
+  }
+  const uint32_t G = gridDim.x, w = blockIdx.x, nblk = p.nblk;
+  const uint64_t tag = p.tag;
+  const uint32_t KW = w < nblk ? (nblk - 1 - w) / G + 1 : 0;  // this workgroup's blocks
+  uint8_t* stage = smem + 2 * Cfg::kBuf;
+  uint32_t* meta = reinterpret_cast<uint32_t*>(smem + 2 * Cfg::kBuf + Cfg::kStage);
+  auto slot_of = [&](uint32_t k) -> uint8_t* { return smem + (k & 1) * Cfg::kBuf; };
+  auto blk_of = [&](uint32_t k) -> uint32_t { return w + k * G; };
+  uint32_t ring_k0 = 0, ring_off = 0, ring_len = 0;
+  auto ring_load = [&](uint32_t k0) {
+    ring_k0 = k0;
+    const uint64_t b = (uint64_t)w + (uint64_t)(k0 + lane) * G;
+    ring_off = b < nblk ? p.blk_off[b] : 0u;
+    ring_len = b < nblk ? p.blk_len[b] : 0u;
+  };
+#ifdef LSMGPU_STAMPS
+  const bool st = p.stamps != nullptr;
+  uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tprev = st ? stamp() : 0;
+  auto mark = [&](int i) {
+    if (st) {
+      const uint64_t t = stamp();
+      acc[i] += t - tprev;
+      tprev = t;
+    }
+  };
+  uint64_t* spec_acc = st ? &acc[6] : nullptr;
+#else
+  auto mark = [](int) {};
+  uint64_t* spec_acc = nullptr;
+#endif
+  BlockRef ref_next{0, 0, 0, false, false};
+  if (KW > 0) {
+    ring_load(0);
+    ref_next = prefetch_block<4096, Cfg::kIters>(p, readlane(ring_off, 0), readlane(ring_len, 0),
+                                                 slot_of(0), lane);
+  }
+  Pend pa, pb, pc;  // blocks k-3, k-2, k-1 (pc: after the walk, block k)
+  uint64_t poll = 0;
+  for (uint32_t k = 0; k < KW + L; k++) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const BlockRef ref = ref_next;
+    mark(0);
+    // b. emit block k - L
+    if (k >= L) {
+      const uint32_t be = blk_of(k - L);
+      Tot ex{0, 0, 0};
+      if (!(p.ablate & 1)) ex = prefix_of(p, be, poll, tag, lane);
+      mark(5);
+      if (be == nblk - 1 && lane == 0) {  // totals of the whole batch
+        const uint32_t n = readlane(pa.sc, 0), K = readlane(pa.sc, 1), V = readlane(pa.sc, 2);
+        if (p.blk_first) p.blk_first[nblk] = ex.n + n;
+        p.result[0] = sat_add(ex.n, n);
+        p.result[1] = sat_add(ex.k, K);
+        p.result[2] = sat_add(ex.v, V);
+      }
+      emit_pend(p, pa, be, ex, lane);
+    }
+    pa = pb;
+    pb = pc;
+    mark(1);
+    // c. next prefix poll, next block's bytes
+    if (k + 1 >= L && k + 1 - L < KW && lane < 3 && !(p.ablate & 1))
+      poll = gload(p.lb + (uint64_t)blk_of(k + 1 - L) * 8 + 4 + lane);
+    if (k + 1 < KW) {
+      if (k + 1 - ring_k0 >= (uint32_t)kWave) ring_load(k + 1);
+      const uint32_t i = k + 1 - ring_k0;
+      ref_next = prefetch_block<4096, Cfg::kIters>(p, readlane(ring_off, i), readlane(ring_len, i),
+                                                   slot_of(k + 1), lane);
+    }
+    mark(2);
+    // d. walk + stage block k
+    if (k < KW) {
+      const uint32_t b = blk_of(k);
+      wave_lds_fence();
+      stage_block<MAXE>(p, ref, slot_of(k), stage, meta, pc, lane, spec_acc);
+      mark(3);
+      if (!(p.ablate & 1))
+        store3(p.lb + (uint64_t)b * 8, tag, readlane(pc.sc, 0), readlane(pc.sc, 1),
+               readlane(pc.sc, 2), lane);
+    }
+    // e. group duty for the PREVIOUS block, one iteration late: its group's aggregates are
+    // published by now (no spinning), and the duty never delays this block's aggregate
+    if (k >= 1 && k - 1 < KW && !(p.ablate & 1)) {
+      const uint32_t b = blk_of(k - 1);
+      const uint32_t g0 = b & ~63u;
+      const uint32_t gsize = (nblk - g0 < 64u) ? (nblk - g0) : 64u;
+      if ((b - g0) == (b / G) % gsize) group_lead(p, b, tag, lane);
+    }
+    mark(4);
+    wave_lds_fence();
+  }
+#ifdef LSMGPU_STAMPS
+  if (st && lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) atomicAdd(reinterpret_cast<unsigned long long*>(p.stamps + i), acc[i]);
+    atomicAdd(reinterpret_cast<unsigned long long*>(p.stamps + 8), (unsigned long long)(KW + L));
+    atomicAdd(reinterpret_cast<unsigned long long*>(p.stamps + 9), 1ull);
+  }
+#endif
 }
 
 // Upper bound on the decode kernels' SGPR count (hipcc -Rpass-analysis=kernel-resource-usage),
 // checked by tests/test_abi.py::test_decode_resource_budget.
 constexpr int kDecodeSgprs = 112;
 
-template <int SLOT, int MAXE, int WPB>
+// Persistent grid = workgroups per CU x CUs, the per-CU count MEASURED once per configuration
+// by a residency census (the occupancy API over-reports on MI355X: 3 x 54,112 B of LDS per CU
+// are admitted by the API but not by the hardware -- scripts/residency_probe.hip).
+// Kernel traits: the LDS-lag kernel for a slot size, the register-lag kernel for 4 KiB.
+template <int SLOT, int MAXE, int NS>
+struct LdsLag {
+  static constexpr int kSlot = SLOT;
+  static constexpr int kLds = DecodeCfg<SLOT, MAXE, NS>::kLds;
+  static constexpr const char* kName = "lds-lag";
+  static void (*kernel())(DecodeParams) { return decode_kernel<SLOT, MAXE, NS>; }
+};
+template <int MAXE, int L>
+struct RegLag {
+  static constexpr int kSlot = 4096;
+  static constexpr int kLds = RegCfg<MAXE>::kLds;
+  static constexpr const char* kName = "reg-lag";
+  static void (*kernel())(DecodeParams) { return decode_reg_kernel<MAXE, L>; }
+};
+
+template <class T>
+static int resident_per_cu(const DecodeParams& p, int num_cus, hipStream_t s) {
+  using Cfg = T;
+  auto k = T::kernel();
+  const int SLOT = T::kSlot;
+  static int per_cu = 0;
+  if (per_cu) return per_cu;
+  if (Cfg::kLds > 64 * 1024 &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::kLds) != hipSuccess)
+    return -1;
+  int api = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&api, k, 64, Cfg::kLds) != hipSuccess) return -1;
+  const int waves_per_simd = 800 / (((kDecodeSgprs + 15) / 16) * 16 + 16);
+  int cand = api;
+  const int lds_bound = (160 * 1024) / Cfg::kLds;
+  if (cand > lds_bound) cand = lds_bound;
+  if (cand > waves_per_simd * 4) cand = waves_per_simd * 4;
+  uint32_t* c = nullptr;
+  if (hipMalloc(&c, 8) != hipSuccess) return -1;
+  int found = 1;
+  for (; cand >= 1; cand--) {
+    const uint32_t grid = (uint32_t)cand * (uint32_t)num_cus;
+    uint32_t h[2] = {0, 0};
+    DecodeParams q = p;
+    q.census = c;
+    q.stamps = nullptr;
+    if (hipMemsetAsync(c, 0, 8, s) != hipSuccess) break;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(64), Cfg::kLds, s, q);
+    if (hipMemcpyAsync(h, c + 0, 8, hipMemcpyDeviceToHost, s) != hipSuccess) break;
+    if (hipStreamSynchronize(s) != hipSuccess) break;
+    if (h[1] == grid) {
+      found = cand;
+      break;
+    }
+  }
+  (void)hipFree(c);
+  per_cu = found;
+  if (getenv("LSMGPU_DEBUG"))
+    fprintf(stderr, "[lsmgpu] decode SLOT=%d census: api %d lds %d -> resident %d per CU\n", SLOT,
+            api, Cfg::kLds, per_cu);
+  return per_cu;
+}
+
+template <class T>
 static hipError_t launch_cfg(const DecodeParams& p, int num_cus, hipStream_t s,
                              uint64_t* waves_launched) {
-  using Cfg = DecodeCfg<SLOT, MAXE, WPB>;
-  auto k = decode_kernel<SLOT, MAXE, WPB>;
-  static int per_cu = 0;
-  if (per_cu == 0) {
-    if (Cfg::kLds > 64 * 1024) {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::kLds);
-      if (e != hipSuccess) return e;
-    }
-    // residency = min(occupancy API, LDS, SGPR-file bound) (MI355X_MICROARCH: the API can
-    // over-report by one block per CU for SGPR-heavy kernels)
-    int api = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&api, k, WPB * 64, Cfg::kLds);
-    if (e != hipSuccess) return e;
-    const int waves_per_simd = 800 / (((kDecodeSgprs + 15) / 16) * 16 + 16);
-    const int waves_per_cu = (waves_per_simd > 8 ? 8 : waves_per_simd) * 4;
-    const int sg_bound = waves_per_cu / WPB;
-    const int lds_bound = (160 * 1024) / Cfg::kLds;
-    per_cu = api;
-    if (per_cu > lds_bound) per_cu = lds_bound;
-    if (per_cu > sg_bound) per_cu = sg_bound;
-    if (per_cu < 1) per_cu = 1;
-  }
-  // a multiple of 64 workgroups (each 64-tile group sits in one round), never more than what
-  // is resident at once, never more than the tiles
+  using Cfg = T;
+  auto k = T::kernel();
+  const int per_cu = resident_per_cu<T>(p, num_cus, s);
+  if (per_cu < 1) return hipErrorLaunchFailure;
+  // a multiple of 64 workgroups (each 64-block group sits in one round), never more than what
+  // is resident at once, never more than the blocks
   uint64_t grid = (uint64_t)per_cu * (uint64_t)num_cus;
   grid = grid / 64 * 64;
   if (grid < 64) grid = 64;
-  const uint64_t ntiles = ((uint64_t)p.nblk + WPB - 1) / WPB;
-  if (grid > ntiles) grid = ntiles;  // one round: every tile has its own workgroup
+  // LSMGPU_GRID (tests/diagnostics): a smaller multiple of 64 workgroups -> many rounds
+  const uint64_t grid_cap = getenv("LSMGPU_GRID") ? (uint64_t)atoll(getenv("LSMGPU_GRID")) : 0;
+  if (grid_cap >= 64 && grid_cap / 64 * 64 < grid) grid = grid_cap / 64 * 64;
+  if (grid > p.nblk) grid = p.nblk;  // one round: every block has its own workgroup
   if (grid < 1) grid = 1;
-  *waves_launched = grid * WPB;
-  static const bool dbg = getenv("LSMGPU_DEBUG") != nullptr;
+  *waves_launched = grid;
   static const uint32_t ablate =
       getenv("LSMGPU_ABLATE") ? (uint32_t)atoi(getenv("LSMGPU_ABLATE")) : 0u;
   DecodeParams q = p;
   q.ablate = ablate;
-  if (dbg)
-    fprintf(stderr, "[lsmgpu] decode SLOT=%d MAXE=%d WPB=%d lds=%d per_cu=%d cus=%d grid=%llu nblk=%u\n",
-            SLOT, MAXE, WPB, Cfg::kLds, per_cu, num_cus, (unsigned long long)grid, p.nblk);
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(WPB * 64), Cfg::kLds, s, q);
-  return hipGetLastError();
+  q.census = nullptr;
+  q.stamps = nullptr;
+  static uint64_t* stamps = nullptr;
+  const bool want_stamps = getenv("LSMGPU_STAMPS") != nullptr;
+  if (want_stamps) {
+    if (!stamps && hipMalloc(&stamps, 16 * sizeof(uint64_t)) != hipSuccess) stamps = nullptr;
+    if (stamps) {
+      (void)hipMemsetAsync(stamps, 0, 16 * sizeof(uint64_t), s);
+      q.stamps = stamps;
+    }
+  }
+  if (getenv("LSMGPU_DEBUG"))
+    fprintf(stderr, "[lsmgpu] decode %s SLOT=%d lds=%d per_cu=%d cus=%d grid=%llu nblk=%u\n",
+            T::kName, T::kSlot, Cfg::kLds, per_cu, num_cus, (unsigned long long)grid, p.nblk);
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64), Cfg::kLds, s, q);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && q.stamps) {
+    uint64_t h[16] = {0};
+    (void)hipMemcpyAsync(h, stamps, sizeof(h), hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
+    const double it = h[8] ? (double)h[8] : 1.0;
+    fprintf(stderr, "[lsmgpu] stamps per wave-iteration (s_memtime cycles): drain %.0f prefix-wait %.0f "
+            "emit %.0f issue %.0f walk %.0f (spec %.0f, meta %.0f, rounds %.2f) publish %.0f | "
+            "iterations %llu waves %llu\n", h[0] / it, h[5] / it, h[1] / it, h[2] / it, h[3] / it,
+            h[6] / it, (h[3] - h[6]) / it, h[7] / it, h[4] / it, (unsigned long long)h[8],
+            (unsigned long long)h[9]);
+  }
+  return e;
 }
 
 hipError_t launch_decode(const DecodeParams& p, uint32_t max_blk_len, int num_cus,
                          hipStream_t s, uint64_t* waves_launched) {
-  if (max_blk_len <= 4096) return launch_cfg<4096, 128, 4>(p, num_cus, s, waves_launched);
-  if (max_blk_len <= 8192) return launch_cfg<8192, 256, 4>(p, num_cus, s, waves_launched);
-  if (max_blk_len <= 16384) return launch_cfg<16384, 512, 2>(p, num_cus, s, waves_launched);
+  static const bool lds_lag_4k = getenv("LSMGPU_LDS_LAG_4K") != nullptr;  // A/B diagnostics
+  if (max_blk_len <= 4096 && !lds_lag_4k) return launch_cfg<RegLag<128, 3>>(p, num_cus, s, waves_launched);
+  if (max_blk_len <= 4096) return launch_cfg<LdsLag<4096, 100, 4>>(p, num_cus, s, waves_launched);
+  if (max_blk_len <= 8192) return launch_cfg<LdsLag<8192, 256, 4>>(p, num_cus, s, waves_launched);
+  if (max_blk_len <= 16384) return launch_cfg<LdsLag<16384, 512, 3>>(p, num_cus, s, waves_launched);
   // 32 KiB slot; larger blocks run the global-memory path inside the same kernel
-  return launch_cfg<32768, 1024, 1>(p, num_cus, s, waves_launched);
+  return launch_cfg<LdsLag<32768, 1024, 3>>(p, num_cus, s, waves_launched);
 }
 
 }  // namespace lsmgpu

@@ -5,8 +5,9 @@
 
 namespace lsmgpu {
 
-// Decode: one wave per SST data block over a persistent, fully resident grid; output bases
-// from a two-level prefix over per-block {entries, key bytes, value bytes}.  DESIGN.md.
+// Decode: one-wave workgroups over a persistent, fully resident grid, one SST data block per
+// iteration, software-pipelined (walk block k, emit block k-2); output bases from a two-level
+// prefix over per-block {entries, key bytes, value bytes}.  DESIGN.md.
 struct DecodeParams {
   const uint8_t* data;
   uint64_t data_len;
@@ -30,6 +31,8 @@ struct DecodeParams {
   uint64_t* result;         // 8 u64, zeroed before launch
   uint32_t tag;             // 24-bit epoch tag of this launch
   uint32_t ablate;          // timing-only diagnostics (LSMGPU_ABLATE): 1 no prefix, 2 no emit, 4 no walk
+  uint32_t* census;         // residency census mode (launch_decode calibration), else nullptr
+  uint64_t* stamps;         // per-phase s_memtime totals (LSMGPU_STAMPS diagnostics), else nullptr
 };
 
 // Encode: one wave per output block; every byte position is closed-form

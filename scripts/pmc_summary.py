@@ -1,16 +1,19 @@
-"""Per-block instruction counts of the decode kernel from a rocprofv3 --pmc CSV."""
-import collections
+"""Per-kernel mean of every PMC counter in rocprofv3 counter_collection CSVs."""
 import csv
 import sys
+from collections import defaultdict
 
-rows = list(csv.DictReader(open(sys.argv[1])))
-nblk = int(sys.argv[2]) if len(sys.argv) > 2 else 256991
-by = collections.defaultdict(dict)
-for r in rows:
-    if "decode_kernel" in r["Kernel_Name"]:
-        by[r["Dispatch_Id"]][r["Counter_Name"]] = float(r["Counter_Value"])
-        by[r["Dispatch_Id"]]["_us"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-v = list(by.values())[-1]
-print("kernel us %.1f  per block: VALU %.0f SALU %.0f LDS %.0f VMEM %.0f" % (
-    v["_us"], v["SQ_INSTS_VALU"] / nblk, v["SQ_INSTS_SALU"] / nblk, v["SQ_INSTS_LDS"] / nblk,
-    v["SQ_INSTS_VMEM"] / nblk))
+for path in sys.argv[1:]:
+    agg = defaultdict(lambda: defaultdict(float))
+    disp = defaultdict(set)
+    for r in csv.DictReader(open(path)):
+        k = r["Kernel_Name"].split("(")[0][:70]
+        agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        disp[k].add(r["Dispatch_Id"])
+    for k, v in agg.items():
+        if "decode" not in k:
+            continue
+        n = len(disp[k])
+        print(path, k, "dispatches", n)
+        for c in sorted(v):
+            print(f"   {c:24s} {v[c] / n:16.0f}")

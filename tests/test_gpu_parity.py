@@ -243,3 +243,43 @@ def test_encode_rejects_bad_keys(codec):
     ve = np.array([3], np.uint32)
     with pytest.raises(LsmgpuError):
         codec.encode_host(kb, ke, vb, ve, 100, 0)
+
+
+def _random_cols(n, seed, kmin=9, kmax=40, vmin=3, vmax=60):
+    """Sorted-irrelevant random columns: key lengths kmin..kmax, vs lengths vmin..vmax (the
+    decoder does not care about order); many short entries -> many entries per 4 KiB block."""
+    rng = np.random.default_rng(seed)
+    kl = rng.integers(kmin, kmax + 1, n)
+    vl = rng.integers(vmin, vmax + 1, n)
+    keys = rng.integers(0, 256, int(kl.sum()), dtype=np.uint8)
+    vs = rng.integers(0, 256, int(vl.sum()), dtype=np.uint8)
+    return keys, np.cumsum(kl).astype(np.uint32), vs, np.cumsum(vl).astype(np.uint32)
+
+
+@pytest.mark.parametrize("grid", [64, 128])
+@pytest.mark.parametrize("shape", ["c2", "c3", "c5", "short", "mixed"])
+def test_many_rounds(codec, oracle, monkeypatch, grid, shape):
+    """The persistent grid capped (LSMGPU_GRID) so a modest batch runs many rounds: the
+    software-pipelined emit (tile k-1 written after tile k is walked), the group look-back
+    across rounds and the LDS slot ring all get exercised, for every slot configuration."""
+    monkeypatch.setenv("LSMGPU_GRID", str(grid))
+    if shape == "c2":
+        c = _cols(2, 150000, seed=7)
+        cols, epb, bb = (c.keys, c.key_end, c.vs, c.vs_end), 0, 4096
+    elif shape == "c3":
+        c = _cols(3, 20000, seed=7)
+        cols, epb, bb = (c.keys, c.key_end, c.vs, c.vs_end), 0, 4096
+    elif shape == "c5":
+        c = _cols(5, 60000, seed=7)
+        cols, epb, bb = (c.keys, c.key_end, c.vs, c.vs_end), c.entries_per_block, c.block_bytes
+    elif shape == "short":  # ~90-180 entries per 4 KiB block, keys/values often < 16 B
+        cols, epb, bb = _random_cols(200000, 11), 0, 4096
+    else:                   # 8 KiB-slot batch: 100 entries/block of 9..60 B keys, 3..100 B values
+        cols, epb, bb = _random_cols(100000, 12, 9, 60, 3, 100), 100, 0
+    sst, _, _ = oracle.build_cols(*cols, epb, bb)
+    sst = sst + b"{}" + (2).to_bytes(4, "big")
+    off, ln, _, _ = oracle.parse_index(sst)
+    g = codec.decode_host(sst, off, ln)
+    _assert_same(g, oracle.decode(sst, off, ln), f"{shape} grid={grid}")
+    assert g.key_data.tobytes() == cols[0].tobytes()
+    assert g.val_data.tobytes() == cols[2].tobytes()
