@@ -28,6 +28,7 @@ def build_lib(force: bool = False, verbose: bool = True) -> str:
            "-o", LIB] + [os.path.join(CSRC, s) for s in SOURCES]
     if os.environ.get("LSMGPU_BUILD_STAMPS"):  # diagnostic build: per-phase s_memtime stamps
         cmd.insert(1, "-DLSMGPU_STAMPS")
+        cmd[cmd.index(LIB)] = LIB.replace("liblsmgpu.so", "liblsmgpu_stamps.so")
     if verbose:
         print("[build]", " ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=CSRC)

@@ -38,12 +38,16 @@ struct LdsSrc {
   const uint8_t* slot;  // 16-B aligned LDS slot (block byte 0 at slot + sh)
   uint32_t sh;
   __device__ __forceinline__ Hdr hdr(uint32_t pos) const {
-    // one unaligned ds_read_b64 (gfx950 runs in unaligned-access mode): plen klen vlen prev.hi
-    uint2 w;
-    __builtin_memcpy(&w, slot + sh + pos, 8);
+    // three ALIGNED dword reads + v_alignbyte: a misaligned ds_read_b64/b128 costs ~10x the
+    // LDS cycles of an aligned one on gfx950 (scripts/lds_probe.hip)
+    const uint32_t p = sh + pos;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(slot + (p & ~3u));
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+    const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, p & 3u);  // plen:klen (BE)
+    const uint32_t x1 = __builtin_amdgcn_alignbyte(w2, w1, p & 3u);  // vlen:..   (BE)
     // v_perm byte selects: BE u16 -> u32
-    return Hdr{__builtin_amdgcn_perm(0u, w.x, 0x0c0c0001u), __builtin_amdgcn_perm(0u, w.x, 0x0c0c0203u),
-               __builtin_amdgcn_perm(0u, w.y, 0x0c0c0001u)};
+    return Hdr{__builtin_amdgcn_perm(0u, x0, 0x0c0c0001u), __builtin_amdgcn_perm(0u, x0, 0x0c0c0203u),
+               __builtin_amdgcn_perm(0u, x1, 0x0c0c0001u)};
   }
 };
 struct GlobalSrc {
@@ -125,6 +129,8 @@ struct SpecResult {
   uint32_t n, status, stop;  // stop = position just after the last entry (its successor's header)
   bool any_plen;
   uint32_t rounds;
+  uint32_t kacc;             // per lane: key bytes (plen + klen) of the entries this lane confirmed
+  uint32_t kst;              // per lane: stored key bytes (klen) of those entries
 };
 // Status of the iterator at a position where no entry was confirmed.
 __device__ __forceinline__ uint32_t stop_status(const LdsSrc& src, uint32_t pf, uint32_t len,
@@ -142,16 +148,17 @@ __device__ __forceinline__ SpecResult walk_spec(const uint8_t* slot, uint32_t sh
                                                 uint32_t* meta, uint32_t maxe, uint32_t lane) {
   const LdsSrc src{slot, sh};
   // first entry (uniform): defines baseKey (iterator.go:129-133) and the first stride guess
-  if (len < 10) return SpecResult{0, stop_status(src, 0, len, 10, true), 0, false, 0};
+  if (len < 10) return SpecResult{0, stop_status(src, 0, len, 10, true), 0, false, 0, 0, 0};
   const Hdr h0 = src.hdr(0);
   const uint32_t base_pos = 10;
   const uint32_t sz0 = 10 + h0.klen + h0.vlen;
   if ((h0.klen | h0.plen) == 0 || h0.plen != 0 || sz0 > len)
-    return SpecResult{0, stop_status(src, 0, len, base_pos, true), 0, false, 0};
+    return SpecResult{0, stop_status(src, 0, len, base_pos, true), 0, false, 0, 0, 0};
   if (lane == 0 && maxe > 0) meta[0] = h0.klen << 16;
   uint32_t pos = sz0, stride = sz0, n = 1;
   bool any_plen = false;
   uint32_t rounds = 0;
+  uint32_t kacc = lane == 0 ? h0.klen : 0u, kst = kacc;
   for (;;) {
     rounds++;
     // lane i checks the entry guessed at pos + i*stride (branch-free)
@@ -166,6 +173,8 @@ __device__ __forceinline__ SpecResult walk_spec(const uint8_t* slot, uint32_t sh
     const uint32_t m = f + ((f < 64 && !fbad) ? 1u : 0u);  // confirmed entries: lanes [0, m)
     const bool conf = lane < m;
     if (conf && n + lane < maxe) meta[n + lane] = p | (h.klen << 16);
+    kacc += conf ? h.plen + h.klen : 0u;
+    kst += conf ? h.klen : 0u;
     any_plen = any_plen || (__ballot(conf && h.plen != 0) != 0);
     n += m;
     if (f == 64) {  // 64 entries of exactly `stride` bytes
@@ -173,7 +182,7 @@ __device__ __forceinline__ SpecResult walk_spec(const uint8_t* slot, uint32_t sh
       continue;
     }
     const uint32_t pf = readlane(p, f);
-    if (fbad) return SpecResult{n, stop_status(src, pf, len, base_pos, false), pf, any_plen, rounds};
+    if (fbad) return SpecResult{n, stop_status(src, pf, len, base_pos, false), pf, any_plen, rounds, kacc, kst};
     const uint32_t szf = readlane(sz, f);  // entry f has another size: continue after it
     pos = pf + szf;
     if (f == 0) stride = szf;  // the guess failed at once: adopt the new size
@@ -186,16 +195,42 @@ struct Plan {
   uint32_t off, len, sh;
   uint32_t kind;
   uint32_t jk, jv;       // log2(lanes per entry) of the key / value streams
+  uint32_t ku;           // the common key length of every entry, 0 if they differ
+  uint32_t big;          // every key and every value is >= 16 B (16-B pieces only)
+  uint32_t jkv;          // log2(lanes per entry) for key + value pieces together
 };
 
 // After walk_spec: meta[e] := header pos | key offset << 16 (wave scan of klen), sentinel
 // meta[n] = stop | K << 16; derives the stream sizes, lanes-per-entry and the 2-run flags.
 // Requires n <= maxe (meta holds maxe + 2 words).
+// Pieces of an entry stream of `len` bytes: 16-B pieces (the last overlapping back inside the
+// entry) from 16 B up; below that two overlapping pieces of the largest power of two <= len.
+__device__ __forceinline__ uint32_t n_pieces(uint32_t len) {
+  return len >= 16 ? (len + 15) >> 4 : (len >= 2 ? 2u : len);
+}
+__device__ __forceinline__ uint32_t piece_log2(uint32_t len) {  // log2 of the piece size
+  return len >= 16 ? 4u : len >= 8 ? 3u : len >= 4 ? 2u : len >= 2 ? 1u : 0u;
+}
+
 __device__ __forceinline__ void finish_meta(uint32_t* meta, const SpecResult& r, uint32_t lane,
                                             Plan& pl) {
   if (lane == 0) meta[r.n] = r.stop;  // klen field 0: the walk's successor position
   wave_lds_fence();
-  uint32_t K = 0, kmax = 0, vmax = 0;
+  uint32_t K = 0, kl0 = 0;
+  bool nonuni = false, small = false;
+  uint32_t jk = 0, jv = 0, jkv = 0;
+  // lanes per entry = pieces of the longest entry, rounded up to a power of two (ballots)
+  auto jl_of = [](uint32_t len, bool on) -> uint32_t {
+    const uint32_t pc = len >= 16 ? (len + 15) >> 4 : 2u;
+    uint32_t j = 0;
+    j = __ballot(on && pc > 1) ? 1u : j;
+    j = __ballot(on && pc > 2) ? 2u : j;
+    j = __ballot(on && pc > 4) ? 3u : j;
+    j = __ballot(on && pc > 8) ? 4u : j;
+    j = __ballot(on && pc > 16) ? 5u : j;
+    j = __ballot(on && pc > 32) ? 6u : j;
+    return j;
+  };
   for (uint32_t e0 = 0; e0 < r.n; e0 += kWave) {
     const uint32_t e = e0 + lane;
     const bool on = e < r.n;
@@ -208,24 +243,23 @@ __device__ __forceinline__ void finish_meta(uint32_t* meta, const SpecResult& r,
     wave_lds_fence();  // every lane has read meta[e + 1] before it is rewritten
     if (on) meta[e] = p | ((K + inc - kl) << 16);
     K += ksum;
-    kmax = max(kmax, kl);
-    vmax = max(vmax, vl);
+    if (e0 == 0) kl0 = readlane(kl, 0);
+    nonuni = nonuni || __ballot(on && kl != kl0) != 0;
+    small = small || __ballot(on && (kl < 16 || vl < 16)) != 0;
+    jk = max(jk, jl_of(kl, on));
+    jv = max(jv, jl_of(vl, on));
+    jkv = max(jkv, jl_of(16 * (n_pieces(kl) + n_pieces(vl)), on));
   }
-  kmax = wave_max(kmax);
-  vmax = wave_max(vmax);
   if (lane == 0) meta[r.n] = r.stop | (K << 16);
   wave_lds_fence();
   pl.n = r.n;
   pl.K = K;
   pl.V = r.stop - 10 * r.n - K;
-  auto jlog = [](uint32_t mx) -> uint32_t {  // lanes per entry: pieces of the longest entry
-    const uint32_t c = mx >= 16 ? (mx + 15) / 16 : 2u;
-    uint32_t j = 0;
-    while ((1u << j) < c && j < 6) j++;
-    return j;
-  };
-  pl.jk = jlog(kmax);
-  pl.jv = jlog(vmax);
+  pl.jk = jk;
+  pl.jv = jv;
+  pl.ku = nonuni ? 0u : kl0;
+  pl.big = small ? 0u : 1u;
+  pl.jkv = jkv;
 }
 
 struct Tot {
@@ -540,7 +574,7 @@ __device__ __forceinline__ void land_tail(const DecodeParams& p, const BlockRef&
 }
 
 // Walk one block (its bytes already in `slot` when it fits): the emit plan + meta.
-template <int SLOT, int MAXE>
+template <int SLOT, int MAXE, bool NO_GLOBAL = false>
 __device__ __forceinline__ Plan walk_stage(const DecodeParams& p, const BlockRef& ref, bool valid,
                                            uint8_t* slot, uint32_t* meta, uint32_t lane,
                                            uint64_t* spec_acc = nullptr) {
@@ -573,7 +607,15 @@ __device__ __forceinline__ Plan walk_stage(const DecodeParams& p, const BlockRef
       pl.kind = pl.n ? 1u : 0u;
       return pl;
     }
+    if (NO_GLOBAL) {  // counts straight from the walk; the global-memory emit path later
+      pl.n = r.n;
+      pl.K = wave_sum_sat(r.kacc);
+      pl.V = r.stop - 10 * r.n - wave_sum_sat(r.kst);
+      pl.kind = r.n ? 2u : 0u;
+      return pl;
+    }
   }
+  if constexpr (NO_GLOBAL) return pl;  // (never: every block of this kernel fits its slot)
   const WalkResult w = walk_block(GlobalSrc{p.data + ref.off}, ref.len);
   pl.n = w.n;
   pl.K = w.K;
@@ -633,9 +675,9 @@ __device__ __forceinline__ void emit_block(const DecodeParams& p, const Plan& pl
 
 // The walk's plan of a block, parked in LDS next to its metadata until the block is emitted
 // (two iterations later).
-constexpr int kPlanWords = 10;
+constexpr int kPlanWords = 12;
 __device__ __forceinline__ void plan_store(uint32_t* rec, const Plan& pl, uint32_t lane) {
-  const uint32_t v[kPlanWords] = {pl.n, pl.K, pl.V, pl.status, pl.off, pl.len, pl.sh, pl.kind, pl.jk, pl.jv};
+  const uint32_t v[kPlanWords] = {pl.n, pl.K, pl.V, pl.status, pl.off, pl.len, pl.sh, pl.kind, pl.jk, pl.jv, pl.ku, pl.big};
   if (lane < (uint32_t)kPlanWords) {
     uint32_t x = v[0];
 #pragma unroll
@@ -655,6 +697,8 @@ __device__ __forceinline__ Plan plan_load(const uint32_t* rec) {
   pl.kind = uniform(rec[7]);
   pl.jk = uniform(rec[8]);
   pl.jv = uniform(rec[9]);
+  pl.ku = uniform(rec[10]);
+  pl.big = uniform(rec[11]);
   return pl;
 }
 
@@ -813,10 +857,21 @@ __global__ void __launch_bounds__(64) decode_kernel(DecodeParams p) {
 // plus the per-entry end offsets, with no LDS traffic.
 constexpr int kRegChunks = 5;  // 320 chunks per block >= (4096 + 16 + 16) / 16
 struct Pend {
-  uint4 c[kRegChunks];          // chunk q = 64 s + lane of [key stream | value stream]
-  uint32_t m0, m0n, m1, m1n;    // meta words of entries lane, lane + 1, 64 + lane, 65 + lane
-  uint32_t sc;                  // lane i = field i: n, K, V, status, off, len, kind
+  uint4 c[kRegChunks];          // chunk mode: chunk q = 64 s + lane of [key stream | value stream]
+                                // piece mode: this lane's s-th 16-B piece
+  uint32_t po[kRegChunks];      // piece mode: stream offset of the piece | kValueBit, or kNoPiece
+  uint32_t end0, end1;          // entries lane, 64 + lane: key end | value end << 16 (in-block)
+  uint32_t sc;                  // lane i = field i: n, K, V, status, off, len, kind, mode
 };
+constexpr uint32_t kValueBit = 0x80000000u;
+constexpr uint32_t kNoPiece = 0xffffffffu;
+
+// Entry e's exclusive ends within its block: key end | value end << 16 (both < 4 KiB).
+__device__ __forceinline__ uint32_t ends_word(const uint32_t* meta, uint32_t e) {
+  const uint32_t w1 = meta[e + 1];
+  const uint32_t k1 = w1 >> 16, vo1 = (w1 & 0xffffu) - 10 * (e + 1) - k1;
+  return (k1 & 0xffffu) | (vo1 << 16);
+}
 
 template <int MAXE>
 struct RegCfg {
@@ -825,7 +880,8 @@ struct RegCfg {
   static constexpr int kBuf = kSlot + 16;
   static constexpr int kStage = kSlot + 32;
   static constexpr int kMetaWords = MAXE + 2;
-  static constexpr int kLds = 2 * kBuf + kStage + kMetaWords * 4;
+  static constexpr int kMetaBytes = (kMetaWords * 4 + 15) & ~15;
+  static constexpr int kLds = kMetaBytes + kStage + 2 * kBuf;
   static constexpr int kIters = (kSlot + 16 + 16 * kWave - 1) / (16 * kWave);
 };
 
@@ -833,62 +889,264 @@ __device__ __forceinline__ uint32_t chunk_off(uint32_t q, uint32_t Q, uint32_t L
   return q + 1 == Q ? L - 16 : 16 * q;  // the last chunk overlaps back inside the stream
 }
 
+// Bytes [0, x) from a, [x, 16) from b (0 <= x <= 16).
+__device__ __forceinline__ uint32_t lo_mask(int32_t x, int32_t d) {
+  int32_t sft = 32 - 8 * (x - 4 * d);  // bytes of dword d below x -> keep mask
+  sft = sft < 0 ? 0 : (sft > 32 ? 32 : sft);
+  return (uint32_t)(0xffffffffull >> sft);
+}
+__device__ __forceinline__ uint4 blend_at(const uint4& a, const uint4& b, int32_t x) {
+  uint4 r;
+  uint32_t m;
+  m = lo_mask(x, 0); r.x = (a.x & m) | (b.x & ~m);
+  m = lo_mask(x, 1); r.y = (a.y & m) | (b.y & ~m);
+  m = lo_mask(x, 2); r.z = (a.z & m) | (b.z & ~m);
+  m = lo_mask(x, 3); r.w = (a.w & m) | (b.w & ~m);
+  return r;
+}
+
+// One stream (keys or values) of one block assembled into `stage` (16-B aligned) as aligned
+// 16-B chunks: chunk q = stream bytes [16q, 16q + 16).  Entry e owns the chunks whose first
+// byte lies in [o(e), o(e+1)); J = 2^jl lanes per entry.  A chunk is one dword-aligned
+// window of its owner (5 ds_read_b32 + v_alignbyte; `win` has >= 16 addressable bytes before
+// the block) blended at the entry boundary with its successor's window (`two`: every entry
+// >= 16 B, so two runs suffice) or run by run (general).  Every LDS access is aligned.
+template <bool IS_KEY>
+__device__ __forceinline__ void assemble_stream(uint8_t* stage, const uint8_t* win, uint32_t wsh,
+                                                const uint32_t* meta, uint32_t n, uint32_t L,
+                                                uint32_t jl, bool two, uint32_t lane) {
+  const uint32_t Q = (L + 15) >> 4;
+  const uint32_t J = 1u << jl;
+  const uint32_t epi = kWave >> jl;
+  const uint32_t j0 = lane & (J - 1);
+  if (two && jl < 6) {
+    // every entry >= 16 B and <= J chunks per entry: batches of NB entries per lane.  Every
+    // LDS read is UNCONDITIONAL (indices clamped into [0, n]; results selected afterwards):
+    // a read under a divergent branch gets its own lgkmcnt wait and serialises the batch.
+    constexpr int NB = 2;
+    for (uint32_t e0 = 0; e0 < n; e0 += NB * epi) {
+      uint32_t m0[NB], m1[NB], m2[NB], eidx[NB];
+#pragma unroll
+      for (int i = 0; i < NB; i++) {
+        const uint32_t e = e0 + i * epi + (lane >> jl);
+        eidx[i] = e;
+        const uint32_t ec = min(e, n - 1);
+        m0[i] = meta[ec];
+        m1[i] = meta[ec + 1];
+        m2[i] = meta[min(ec + 2, n)];
+      }
+      uint32_t t0[NB], x[NB], a1[NB], a2[NB];
+      bool on[NB];
+#pragma unroll
+      for (int i = 0; i < NB; i++) {
+        const uint32_t e = eidx[i];
+        const uint32_t p0 = m0[i] & 0xffffu, k0 = m0[i] >> 16, p1 = m1[i] & 0xffffu,
+                       k1 = m1[i] >> 16, k2 = m2[i] >> 16;
+        uint32_t o, o1, sp, s1;
+        if (IS_KEY) {
+          o = k0;
+          o1 = k1;
+          sp = p0 + 10;
+          s1 = p1 + 10;
+        } else {
+          o = p0 - 10 * e - k0;
+          o1 = p1 - 10 * (e + 1) - k1;
+          sp = p0 + 10 + (k1 - k0);
+          s1 = p1 + 10 + (k2 - k1);
+        }
+        const uint32_t qa = (o + 15) >> 4;
+        const uint32_t qb = (e + 1 >= n) ? Q : (o1 + 15) >> 4;
+        const uint32_t q = qa + j0;
+        on[i] = e < n && q < qb;
+        t0[i] = 16 * q;
+        const int32_t xi = (int32_t)o1 - (int32_t)(16 * q);
+        x[i] = (e + 1 >= n || xi >= 16) ? 16u : (uint32_t)xi;
+        a1[i] = on[i] ? wsh + sp + (16 * q - o) : wsh;
+        a2[i] = on[i] && x[i] < 16 ? wsh + s1 - x[i] : wsh;
+      }
+      uint4 w1[NB], w2[NB];
+#pragma unroll
+      for (int i = 0; i < NB; i++) {
+        w1[i] = lds_u128(win, a1[i]);
+        w2[i] = lds_u128(win, a2[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < NB; i++)
+        if (on[i]) *reinterpret_cast<uint4*>(stage + t0[i]) = blend_at(w1[i], w2[i], (int32_t)x[i]);
+    }
+    return;
+  }
+  for (uint32_t e0 = 0; e0 < n; e0 += epi) {
+    const uint32_t e = e0 + (lane >> jl);
+    if (e >= n) continue;
+    uint32_t o, o1, sp;
+    entry_span<IS_KEY>(meta, e, o, o1, sp);
+    const uint32_t qa = (o + 15) >> 4;
+    const uint32_t qb = (e + 1 == n) ? Q : (o1 + 15) >> 4;
+    for (uint32_t q = qa + j0; q < qb; q += J) {
+      const uint32_t t0 = 16 * q;  // >= o
+      uint4 v;
+      if (two) {
+        const uint4 w1 = lds_u128(win, wsh + sp + (t0 - o));
+        const int32_t x = (int32_t)o1 - (int32_t)t0;
+        if (x >= 16 || e + 1 >= n) {
+          v = w1;
+        } else {
+          uint32_t oo, oo1, s1;
+          entry_span<IS_KEY>(meta, e + 1, oo, oo1, s1);
+          const uint4 w2 = lds_u128(win, wsh + s1 - (uint32_t)x);
+          v = blend_at(w1, w2, x);
+        }
+      } else {  // general: entries shorter than 16 B, run by run
+        v = make_uint4(0, 0, 0, 0);
+        uint32_t ee = e, eo = o, eo1 = o1, es = sp;
+        uint32_t t = t0;
+        const uint32_t hi = min(t0 + 16, L);
+        while (t < hi) {
+          while (eo1 <= t) {
+            ee++;
+            entry_span<IS_KEY>(meta, ee, eo, eo1, es);
+          }
+          const uint4 w = lds_u128(win, wsh + es + (t0 - eo));
+          const uint32_t rend = min(eo1, hi);
+          v = blend_at(blend_at(v, w, (int32_t)(t - t0)), v, (int32_t)(rend - t0));
+          t = rend;
+        }
+      }
+      *reinterpret_cast<uint4*>(stage + t0) = v;  // aligned ds_write_b128
+    }
+  }
+}
+
 // Walk + stage block k: fills `pd` (registers) from the block in `slot`.
 template <int MAXE>
 __device__ __forceinline__ void stage_block(const DecodeParams& p, const BlockRef& ref,
                                             uint8_t* slot, uint8_t* stage, uint32_t* meta,
                                             Pend& pd, uint32_t lane, uint64_t* spec_acc) {
-  Plan pl = walk_stage<4096, MAXE>(p, ref, true, slot, meta, lane, spec_acc);
+#ifdef LSMGPU_STAMPS
+  uint64_t t0 = spec_acc ? __builtin_amdgcn_s_memtime() : 0;
+  auto sub = [&](int i) {
+    if (spec_acc) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      spec_acc[i] += t - t0;
+      t0 = t;
+    }
+  };
+#else
+  auto sub = [](int) {};
+#endif
+  Plan pl = walk_stage<4096, MAXE, true>(p, ref, true, slot, meta, lane, spec_acc);
+  sub(2);
   if (pl.kind == 1 && (pl.n > 128 || pl.K < 16 || pl.V < 16)) pl.kind = 2;  // n, K, V exact
-  const uint32_t f[7] = {pl.n, pl.K, pl.V, pl.status, pl.off, pl.len, pl.kind};
+  // piece mode: every entry >= 16 B and its key + value pieces (one group of J = 2^jkv lanes
+  // per entry) fit kRegChunks passes
+  const uint32_t passes = pl.jkv < 6 ? (pl.n + (kWave >> pl.jkv) - 1) >> (6 - pl.jkv) : 99u;
+  const uint32_t mode = (pl.kind == 1 && passes <= (uint32_t)kRegChunks) ? 1u : 0u;
+  const uint32_t f[8] = {pl.n, pl.K, pl.V, pl.status, pl.off, pl.len, pl.kind, mode};
   uint32_t x = f[0];
 #pragma unroll
-  for (int i = 1; i < 7; i++) x = lane == (uint32_t)i ? f[i] : x;
+  for (int i = 1; i < 8; i++) x = lane == (uint32_t)i ? f[i] : x;
   pd.sc = x;
   if (pl.kind != 1) return;
-  const uint8_t* src = slot + pl.sh;
-  emit_pieces<true>(stage, src, meta, pl.n, pl.jk, lane);
-  emit_pieces<false>(stage + pl.K, src, meta, pl.n, pl.jv, lane);
-  wave_lds_fence();
+  if (mode == 1) {
+    // lane group (e, j), e = s * 64 / J + lane / J: pieces j < kpc are entry e's key pieces,
+    // the rest its value pieces.  Piece j of a stream covers entry bytes
+    // [min(16 j, len - 16), +16): the last piece overlaps back inside the entry, so the emit's
+    // unaligned stores never touch a byte outside it.  Every LDS read is unconditional and
+    // dword-aligned (window = 5 ds_read_b32 + v_alignbyte).
+    const uint8_t* wn = slot - 64;
+    const uint32_t ws = pl.sh + 64;
+    const uint32_t jl = pl.jkv;
+#pragma unroll
+    for (int s = 0; s < kRegChunks; s++) {
+      const uint32_t e = (uint32_t)s * (kWave >> jl) + (lane >> jl);
+      const uint32_t j = lane & ((1u << jl) - 1);
+      const uint32_t ec = min(e, pl.n - 1);
+      const uint32_t w0 = meta[ec], w1 = meta[ec + 1];
+      const uint32_t p0 = w0 & 0xffffu, k0 = w0 >> 16, p1 = w1 & 0xffffu, k1 = w1 >> 16;
+      const uint32_t klen = k1 - k0, vlen = p1 - p0 - 10 - klen;
+      const uint32_t kpc = n_pieces(klen);
+      const bool key = j < kpc;
+      const uint32_t jj = key ? j : j - kpc;
+      const uint32_t len = key ? klen : vlen;
+      const uint32_t o = key ? k0 : p0 - 10 * ec - k0;
+      const uint32_t sp = key ? p0 + 10 : p0 + 10 + klen;
+      const uint32_t lg = piece_log2(len), sz = 1u << lg;
+      const bool on = (uint32_t)s < passes && e < pl.n && jj < n_pieces(len);
+      const uint32_t off = min(jj << lg, len - sz);
+      pd.c[s] = lds_u128(wn, ws + (on ? sp + off : 0u));
+      pd.po[s] = on ? ((o + off) | (lg << 28) | (key ? 0u : kValueBit)) : kNoPiece;
+    }
+    pd.end0 = ends_word(meta, lane);
+    pd.end1 = ends_word(meta, 64 + lane);
+    sub(3);
+    return;
+  }
+  // windows may start up to 15 B before block byte 0: `win` = slot - 64 (the slots follow the
+  // meta words and the staging buffer in LDS, so those bytes are addressable)
+  const uint8_t* win = slot - 64;
+  const uint32_t wsh = pl.sh + 64;
   const uint32_t Qk = (pl.K + 15) >> 4, Qv = (pl.V + 15) >> 4;
+  // keys of one length that is a multiple of 16 B (16-B hex keys, 64-B keys, ...) go straight
+  // from the block into registers; otherwise both streams are staged
+  const uint32_t kr = pl.ku >> 4;  // 16-B pieces per key
+  const bool kdirect = pl.ku && (pl.ku & 15) == 0 && (kr & (kr - 1)) == 0;
+  const uint32_t vbase = kdirect ? 0u : 16 * Qk;  // value stream's 16-aligned staging offset
+  if (!(p.ablate & 8)) {  // (timing-only ablation: 8 = no stream assembly)
+    if (!kdirect) assemble_stream<true>(stage, win, wsh, meta, pl.n, pl.K, pl.jk, pl.big, lane);
+    assemble_stream<false>(stage + vbase, win, wsh, meta, pl.n, pl.V, pl.jv, pl.big, lane);
+  }
+  sub(3);
+  if (p.ablate & 16) return;  // (timing-only ablation: 16 = no register readback)
+  wave_lds_fence();
+  const uint32_t ksh = kdirect ? __builtin_ctz(kr) : 0u;
+  // chunk addresses (window coordinates): key chunks straight from the block (kdirect) or
+  // from the staging buffer; value chunks from the staging buffer; each stream's last chunk
+  // overlaps back inside it.  Reads are unconditional (see assemble_stream).
+  const uint32_t sbase = (uint32_t)(stage - win);  // staging byte 0 in window coordinates
+  uint32_t km[kRegChunks];
+#pragma unroll
+  for (int s = 0; s < kRegChunks; s++) km[s] = meta[min((64u * s + lane) >> ksh, pl.n)];
 #pragma unroll
   for (int s = 0; s < kRegChunks; s++) {
     const uint32_t q = 64 * s + lane;
-    uint32_t o = 0;
-    if (q < Qk) o = chunk_off(q, Qk, pl.K);
-    else if (q < Qk + Qv) o = pl.K + chunk_off(q - Qk, Qv, pl.V);
-    uint4 v;
-    __builtin_memcpy(&v, stage + o, 16);
-    pd.c[s] = v;
+    uint32_t a;
+    if (q < Qk)
+      a = kdirect ? wsh + (km[s] & 0xffffu) + 10 + 16 * (q & (kr - 1))
+                  : sbase + (q + 1 < Qk ? 16 * q : pl.K - 16);
+    else if (q < Qk + Qv)
+      a = sbase + vbase + (q - Qk + 1 < Qv ? 16 * (q - Qk) : pl.V - 16);
+    else
+      a = sbase;
+    pd.c[s] = lds_u128(win, a);
   }
-  uint2 w0, w1;
-  __builtin_memcpy(&w0, meta + lane, 8);
-  __builtin_memcpy(&w1, meta + 64 + lane, 8);
-  pd.m0 = w0.x;
-  pd.m0n = w0.y;
-  pd.m1 = w1.x;
-  pd.m1n = w1.y;
+  pd.end0 = ends_word(meta, lane);
+  pd.end1 = ends_word(meta, 64 + lane);
+  sub(4);
 }
 
-// Per-entry end offsets / view record of entry e from its meta words (this, next).
-__device__ __forceinline__ void entry_out(const DecodeParams& p, uint32_t e, uint32_t wm,
-                                          uint32_t wn, Tot ex, uint32_t off, bool mat, bool view) {
-  const uint32_t p0 = wm & 0xffffu, k0 = wm >> 16, p1 = wn & 0xffffu, k1 = wn >> 16;
-  const uint32_t vo1 = p1 - 10 * (e + 1) - k1;
+// Per-entry end offsets / view record of entry e from its ends word and its predecessor's.
+__device__ __forceinline__ void entry_out(const DecodeParams& p, uint32_t e, uint32_t we,
+                                          uint32_t wprev, Tot ex, uint32_t off, bool mat,
+                                          bool view) {
+  const uint32_t k1 = we & 0xffffu, vo1 = we >> 16;
   if (mat) {
     if (p.key_end) p.key_end[ex.n + e] = ex.k + k1;
     if (p.val_end) p.val_end[ex.n + e] = ex.v + vo1;
   }
   if (view) {
-    const uint32_t klen = k1 - k0, vlen = vo1 - (p0 - 10 * e - k0);
-    p.view[ex.n + e] = (uint64_t)(off + p0 + 10) | ((uint64_t)klen << 32) | ((uint64_t)vlen << 48);
+    const uint32_t k0 = e ? (wprev & 0xffffu) : 0u, vo0 = e ? (wprev >> 16) : 0u;
+    const uint32_t p0 = vo0 + 10 * e + k0;  // header position (vo = pos - 10 e - ko)
+    p.view[ex.n + e] = (uint64_t)(off + p0 + 10) | ((uint64_t)(k1 - k0) << 32) |
+                       ((uint64_t)(vo1 - vo0) << 48);
   }
 }
 
 __device__ __forceinline__ void emit_pend(const DecodeParams& p, const Pend& pd, uint32_t b, Tot ex,
                                           uint32_t lane) {
   const uint32_t n = readlane(pd.sc, 0), K = readlane(pd.sc, 1), V = readlane(pd.sc, 2),
-                 status = readlane(pd.sc, 3), off = readlane(pd.sc, 4), kind = readlane(pd.sc, 6);
+                 status = readlane(pd.sc, 3), off = readlane(pd.sc, 4), kind = readlane(pd.sc, 6),
+                 mode = readlane(pd.sc, 7);
   if (lane == 0) {
     if (p.blk_first) p.blk_first[b] = ex.n;
     if (p.blk_status) p.blk_status[b] = (int32_t)status;
@@ -907,17 +1165,54 @@ __device__ __forceinline__ void emit_pend(const DecodeParams& p, const Pend& pd,
     ok = ok && kend < 0xffffffffull && vend <= 0xffffffffull;
   }
   if (!ok && lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(p.result + 5), 1ull);
+#ifdef LSMGPU_STAMPS
+  if (p.stamps && lane == 0)  // blocks per emit path: [13] chunk mode, [14] piece mode, [15] global
+    atomicAdd(reinterpret_cast<unsigned long long*>(p.stamps + (kind == 2 ? 15 : 13 + mode)), 1ull);
+#endif
   if (!ok || kind == 0 || (p.ablate & 2)) return;
   if (kind == 2) {
     emit_slow(p, p.data + off, n, ex.n, ex.k, ex.v, off, lane);
     return;
   }
-  if (lane < n) entry_out(p, lane, pd.m0, pd.m0n, ex, off, mat, view);
-  if (64 + lane < n) entry_out(p, 64 + lane, pd.m1, pd.m1n, ex, off, mat, view);
+  uint32_t pr0 = 0, pr1 = 0;  // predecessor ends (view mode only)
+  if (view) {
+    pr0 = __shfl_up(pd.end0, 1);
+    pr1 = __shfl_up(pd.end1, 1);
+    if (lane == 0) pr1 = __builtin_amdgcn_readlane(pd.end0, 63);
+  }
+  if (lane < n) entry_out(p, lane, pd.end0, pr0, ex, off, mat, view);
+  if (64 + lane < n) entry_out(p, 64 + lane, pd.end1, pr1, ex, off, mat, view);
   if (!mat) return;
-  const uint32_t Qk = (K + 15) >> 4, Qv = (V + 15) >> 4;
   uint8_t* kd = p.key_data + ex.k;
   uint8_t* vd = p.val_data + ex.v;
+  if (mode == 1) {  // unaligned 16-B piece stores (overlapping only inside one entry)
+#pragma unroll
+    for (int s = 0; s < kRegChunks; s++) {
+      const uint32_t po = pd.po[s];
+      const bool val = (po & kValueBit) != 0;
+      uint8_t* base = val ? p.val_data : p.key_data;
+      if (po != kNoPiece && base) {
+        const uint4 v = pd.c[s];
+        uint8_t* d = (val ? vd : kd) + (po & 0xffffu);
+        const uint32_t lg = (po >> 28) & 7u;
+        if (lg == 4) {
+          __builtin_memcpy(d, &v, 16);
+        } else if (lg == 3) {
+          const uint2 h = make_uint2(v.x, v.y);
+          __builtin_memcpy(d, &h, 8);
+        } else if (lg == 2) {
+          __builtin_memcpy(d, &v.x, 4);
+        } else if (lg == 1) {
+          const uint16_t h = (uint16_t)v.x;
+          __builtin_memcpy(d, &h, 2);
+        } else {
+          *d = (uint8_t)v.x;
+        }
+      }
+    }
+    return;
+  }
+  const uint32_t Qk = (K + 15) >> 4, Qv = (V + 15) >> 4;
 #pragma unroll
   for (int s = 0; s < kRegChunks; s++) {
     const uint32_t q = 64 * s + lane;
@@ -936,7 +1231,7 @@ __device__ __forceinline__ void emit_pend(const DecodeParams& p, const Pend& pd,
 //   c. issue block k+1-L's prefix poll and block k+1's LDS-DMA (the slot of block k-1)
 //   d. walk + stage block k into registers, publish its aggregate, lead its group if due
 template <int MAXE, int L>
-__global__ void __launch_bounds__(64) decode_reg_kernel(DecodeParams p) {
+__global__ void __launch_bounds__(64, 3) decode_reg_kernel(DecodeParams p) {  // <= 168 VGPRs
   static_assert(L == 3, "three named pending slots");
   using Cfg = RegCfg<MAXE>;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -948,9 +1243,9 @@ __global__ void __launch_bounds__(64) decode_reg_kernel(DecodeParams p) {
   const uint32_t G = gridDim.x, w = blockIdx.x, nblk = p.nblk;
   const uint64_t tag = p.tag;
   const uint32_t KW = w < nblk ? (nblk - 1 - w) / G + 1 : 0;  // this workgroup's blocks
-  uint8_t* stage = smem + 2 * Cfg::kBuf;
-  uint32_t* meta = reinterpret_cast<uint32_t*>(smem + 2 * Cfg::kBuf + Cfg::kStage);
-  auto slot_of = [&](uint32_t k) -> uint8_t* { return smem + (k & 1) * Cfg::kBuf; };
+  uint32_t* meta = reinterpret_cast<uint32_t*>(smem);
+  uint8_t* stage = smem + Cfg::kMetaBytes;
+  auto slot_of = [&](uint32_t k) -> uint8_t* { return smem + Cfg::kMetaBytes + Cfg::kStage + (k & 1) * Cfg::kBuf; };
   auto blk_of = [&](uint32_t k) -> uint32_t { return w + k * G; };
   uint32_t ring_k0 = 0, ring_off = 0, ring_len = 0;
   auto ring_load = [&](uint32_t k0) {
@@ -961,7 +1256,7 @@ __global__ void __launch_bounds__(64) decode_reg_kernel(DecodeParams p) {
   };
 #ifdef LSMGPU_STAMPS
   const bool st = p.stamps != nullptr;
-  uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tprev = st ? stamp() : 0;
   auto mark = [&](int i) {
     if (st) {
@@ -1042,6 +1337,7 @@ __global__ void __launch_bounds__(64) decode_reg_kernel(DecodeParams p) {
     for (int i = 0; i < 8; i++) atomicAdd(reinterpret_cast<unsigned long long*>(p.stamps + i), acc[i]);
     atomicAdd(reinterpret_cast<unsigned long long*>(p.stamps + 8), (unsigned long long)(KW + L));
     atomicAdd(reinterpret_cast<unsigned long long*>(p.stamps + 9), 1ull);
+    for (int i = 8; i < 11; i++) atomicAdd(reinterpret_cast<unsigned long long*>(p.stamps + 2 + i), acc[i]);
   }
 #endif
 }
@@ -1157,10 +1453,12 @@ static hipError_t launch_cfg(const DecodeParams& p, int num_cus, hipStream_t s,
     (void)hipStreamSynchronize(s);
     const double it = h[8] ? (double)h[8] : 1.0;
     fprintf(stderr, "[lsmgpu] stamps per wave-iteration (s_memtime cycles): drain %.0f prefix-wait %.0f "
-            "emit %.0f issue %.0f walk %.0f (spec %.0f, meta %.0f, rounds %.2f) publish %.0f | "
-            "iterations %llu waves %llu\n", h[0] / it, h[5] / it, h[1] / it, h[2] / it, h[3] / it,
-            h[6] / it, (h[3] - h[6]) / it, h[7] / it, h[4] / it, (unsigned long long)h[8],
-            (unsigned long long)h[9]);
+            "emit %.0f issue %.0f walk %.0f (spec %.0f, rounds %.2f; reg-lag: walk total %.0f, stage %.0f, "
+            "readback %.0f) publish %.0f | iterations %llu waves %llu\n", h[0] / it, h[5] / it,
+            h[1] / it, h[2] / it, h[3] / it, h[6] / it, h[7] / it, h[10] / it, h[11] / it,
+            h[12] / it, h[4] / it, (unsigned long long)h[8], (unsigned long long)h[9]);
+    fprintf(stderr, "[lsmgpu] blocks by emit path: chunk %llu piece %llu global %llu\n",
+            (unsigned long long)h[13], (unsigned long long)h[14], (unsigned long long)h[15]);
   }
   return e;
 }
