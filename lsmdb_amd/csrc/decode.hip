@@ -63,9 +63,10 @@ struct WalkResult {
   uint32_t n, K, V, status;
 };
 
-// The blockIterator forward walk over global memory (count only; oversize blocks).
-// Values are identical in every lane.
-__device__ __forceinline__ WalkResult walk_block(const GlobalSrc& src, uint32_t len) {
+// The blockIterator forward walk, serial (count only: oversize blocks from global memory,
+// blocks with more entries than the metadata holds from LDS).  Values identical in every lane.
+template <class Src>
+__device__ __forceinline__ WalkResult walk_block(const Src& src, uint32_t len) {
   uint32_t pos = 0, n = 0, K = 0, V = 0, st = LSMGPU_BLK_OK, base_pos = 0;
   bool have_base = false;
   for (;;) {
@@ -129,8 +130,6 @@ struct SpecResult {
   uint32_t n, status, stop;  // stop = position just after the last entry (its successor's header)
   bool any_plen;
   uint32_t rounds;
-  uint32_t kacc;             // per lane: key bytes (plen + klen) of the entries this lane confirmed
-  uint32_t kst;              // per lane: stored key bytes (klen) of those entries
 };
 // Status of the iterator at a position where no entry was confirmed.
 __device__ __forceinline__ uint32_t stop_status(const LdsSrc& src, uint32_t pf, uint32_t len,
@@ -148,44 +147,46 @@ __device__ __forceinline__ SpecResult walk_spec(const uint8_t* slot, uint32_t sh
                                                 uint32_t* meta, uint32_t maxe, uint32_t lane) {
   const LdsSrc src{slot, sh};
   // first entry (uniform): defines baseKey (iterator.go:129-133) and the first stride guess
-  if (len < 10) return SpecResult{0, stop_status(src, 0, len, 10, true), 0, false, 0, 0, 0};
+  if (len < 10) return SpecResult{0, stop_status(src, 0, len, 10, true), 0, false, 0};
   const Hdr h0 = src.hdr(0);
   const uint32_t base_pos = 10;
   const uint32_t sz0 = 10 + h0.klen + h0.vlen;
   if ((h0.klen | h0.plen) == 0 || h0.plen != 0 || sz0 > len)
-    return SpecResult{0, stop_status(src, 0, len, base_pos, true), 0, false, 0, 0, 0};
+    return SpecResult{0, stop_status(src, 0, len, base_pos, true), 0, false, 0};
   if (lane == 0 && maxe > 0) meta[0] = h0.klen << 16;
-  uint32_t pos = sz0, stride = sz0, n = 1;
-  bool any_plen = false;
+  uint32_t pos = sz0, stride = sz0, n = 1, ls = lane * sz0;
+  uint64_t plen_m = 0;
   uint32_t rounds = 0;
-  uint32_t kacc = lane == 0 ? h0.klen : 0u, kst = kacc;
   for (;;) {
     rounds++;
-    // lane i checks the entry guessed at pos + i*stride (branch-free)
-    const uint32_t p = pos + lane * stride;
-    const bool has_hdr = p + 10 <= len;
-    const Hdr h = src.hdr(has_hdr ? p : 0u);
+    // lane i checks the entry guessed at pos + i * stride (branch-free)
+    const uint32_t p = pos + ls;
+    const bool has = p + 10 <= len;
+    const Hdr h = src.hdr(has ? p : 0u);
     const uint32_t sz = 10 + h.klen + h.vlen;
-    const bool bad = !has_hdr || (h.klen | h.plen) == 0 || base_pos + h.plen > len || p + sz > len;
-    const uint64_t any = __ballot(bad || sz != stride);
-    const uint32_t f = any ? (uint32_t)__builtin_ctzll(any) : 64u;
-    const bool fbad = f < 64 && ((__ballot(bad) >> f) & 1ull);
-    const uint32_t m = f + ((f < 64 && !fbad) ? 1u : 0u);  // confirmed entries: lanes [0, m)
+    const bool ok = has & ((h.klen | h.plen) != 0) & (base_pos + h.plen <= len) & (p + sz <= len);
+    const uint64_t okm = __builtin_amdgcn_ballot_w64(ok);
+    const uint64_t run = okm & __builtin_amdgcn_ballot_w64(sz == stride);
+    const uint64_t brk = ~run;  // the first lane that does not continue the run
+    const uint32_t f = brk ? (uint32_t)__builtin_ctzll(brk) : 64u;
+    const uint32_t fok = f < 64 ? (uint32_t)(okm >> f) & 1u : 0u;
+    const uint32_t m = f + fok;  // confirmed entries: lanes [0, m)
     const bool conf = lane < m;
-    if (conf && n + lane < maxe) meta[n + lane] = p | (h.klen << 16);
-    kacc += conf ? h.plen + h.klen : 0u;
-    kst += conf ? h.klen : 0u;
-    any_plen = any_plen || (__ballot(conf && h.plen != 0) != 0);
+    if (conf & (n + lane < maxe)) meta[n + lane] = p | (h.klen << 16);
+    plen_m |= __builtin_amdgcn_ballot_w64(conf & (h.plen != 0));
     n += m;
     if (f == 64) {  // 64 entries of exactly `stride` bytes
       pos += 64 * stride;
       continue;
     }
     const uint32_t pf = readlane(p, f);
-    if (fbad) return SpecResult{n, stop_status(src, pf, len, base_pos, false), pf, any_plen, rounds, kacc, kst};
+    if (!fok) return SpecResult{n, stop_status(src, pf, len, base_pos, false), pf, plen_m != 0, rounds};
     const uint32_t szf = readlane(sz, f);  // entry f has another size: continue after it
     pos = pf + szf;
-    if (f == 0) stride = szf;  // the guess failed at once: adopt the new size
+    if (f == 0) {  // the guess failed at once: adopt the new size
+      stride = szf;
+      ls = lane * szf;
+    }
   }
 }
 
@@ -607,11 +608,12 @@ __device__ __forceinline__ Plan walk_stage(const DecodeParams& p, const BlockRef
       pl.kind = pl.n ? 1u : 0u;
       return pl;
     }
-    if (NO_GLOBAL) {  // counts straight from the walk; the global-memory emit path later
-      pl.n = r.n;
-      pl.K = wave_sum_sat(r.kacc);
-      pl.V = r.stop - 10 * r.n - wave_sum_sat(r.kst);
-      pl.kind = r.n ? 2u : 0u;
+    if (NO_GLOBAL) {  // rare: counts from a serial walk of the LDS copy; global emit path
+      const WalkResult w = walk_block(LdsSrc{slot, ref.sh}, ref.len);
+      pl.n = w.n;
+      pl.K = w.K;
+      pl.V = w.V;
+      pl.kind = w.n ? 2u : 0u;
       return pl;
     }
   }
@@ -859,12 +861,13 @@ constexpr int kRegChunks = 5;  // 320 chunks per block >= (4096 + 16 + 16) / 16
 struct Pend {
   uint4 c[kRegChunks];          // chunk mode: chunk q = 64 s + lane of [key stream | value stream]
                                 // piece mode: this lane's s-th 16-B piece
-  uint32_t po[kRegChunks];      // piece mode: stream offset of the piece | kValueBit, or kNoPiece
+  uint32_t po[(kRegChunks + 1) / 2];  // piece mode, 16 bits per piece: stream offset (12 b) |
+                                      // log2 size << 12 | value stream << 15; 0xffff = none
   uint32_t end0, end1;          // entries lane, 64 + lane: key end | value end << 16 (in-block)
   uint32_t sc;                  // lane i = field i: n, K, V, status, off, len, kind, mode
 };
-constexpr uint32_t kValueBit = 0x80000000u;
-constexpr uint32_t kNoPiece = 0xffffffffu;
+constexpr uint32_t kValueBit = 0x8000u;
+constexpr uint32_t kNoPiece = 0xffffu;
 
 // Entry e's exclusive ends within its block: key end | value end << 16 (both < 4 KiB).
 __device__ __forceinline__ uint32_t ends_word(const uint32_t* meta, uint32_t e) {
@@ -1075,7 +1078,9 @@ __device__ __forceinline__ void stage_block(const DecodeParams& p, const BlockRe
       const bool on = (uint32_t)s < passes && e < pl.n && jj < n_pieces(len);
       const uint32_t off = min(jj << lg, len - sz);
       pd.c[s] = lds_u128(wn, ws + (on ? sp + off : 0u));
-      pd.po[s] = on ? ((o + off) | (lg << 28) | (key ? 0u : kValueBit)) : kNoPiece;
+      const uint32_t f16 = on ? ((o + off) | (lg << 12) | (key ? 0u : kValueBit)) : kNoPiece;
+      if (s & 1) pd.po[s >> 1] |= f16 << 16;
+      else pd.po[s >> 1] = f16;
     }
     pd.end0 = ends_word(meta, lane);
     pd.end1 = ends_word(meta, 64 + lane);
@@ -1188,13 +1193,13 @@ __device__ __forceinline__ void emit_pend(const DecodeParams& p, const Pend& pd,
   if (mode == 1) {  // unaligned 16-B piece stores (overlapping only inside one entry)
 #pragma unroll
     for (int s = 0; s < kRegChunks; s++) {
-      const uint32_t po = pd.po[s];
+      const uint32_t po = (pd.po[s >> 1] >> (16 * (s & 1))) & 0xffffu;
       const bool val = (po & kValueBit) != 0;
       uint8_t* base = val ? p.val_data : p.key_data;
       if (po != kNoPiece && base) {
         const uint4 v = pd.c[s];
-        uint8_t* d = (val ? vd : kd) + (po & 0xffffu);
-        const uint32_t lg = (po >> 28) & 7u;
+        uint8_t* d = (val ? vd : kd) + (po & 0xfffu);
+        const uint32_t lg = (po >> 12) & 7u;
         if (lg == 4) {
           __builtin_memcpy(d, &v, 16);
         } else if (lg == 3) {
@@ -1277,7 +1282,7 @@ __global__ void __launch_bounds__(64, 3) decode_reg_kernel(DecodeParams p) {  //
                                                  slot_of(0), lane);
   }
   Pend pa, pb, pc;  // blocks k-3, k-2, k-1 (pc: after the walk, block k)
-  uint64_t poll = 0;
+  uint64_t poll = 0;  // block k-L's prefix granules, polled one iteration ahead
   for (uint32_t k = 0; k < KW + L; k++) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const BlockRef ref = ref_next;
