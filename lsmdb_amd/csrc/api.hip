@@ -57,6 +57,8 @@ struct lsmgpu_ctx {
   uint32_t tag = 0;
   DevBuf flags;          // encode flags
   DevBuf scan_tmp;
+  DevBuf wsc;            // walk-scan-copy decode scratch (metadata, per-block triples)
+  DevBuf wsc_tmp;        // its scan temporary storage
   // staging for host-memory calls
   DevBuf s_data, s_off, s_len, s_kd, s_ke, s_vd, s_ve, s_view, s_bf, s_bs, s_a, s_b, s_c, s_d;
 };
@@ -117,7 +119,7 @@ void lsmgpu_close(lsmgpu_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
-  DevBuf* bufs[] = {&c->lb, &c->result, &c->flags, &c->scan_tmp, &c->s_data,
+  DevBuf* bufs[] = {&c->lb, &c->result, &c->flags, &c->scan_tmp, &c->wsc, &c->wsc_tmp, &c->s_data,
                     &c->s_off, &c->s_len, &c->s_kd, &c->s_ke, &c->s_vd, &c->s_ve, &c->s_view,
                     &c->s_bf, &c->s_bs, &c->s_a, &c->s_b, &c->s_c, &c->s_d};
   for (DevBuf* b : bufs) b->release();
@@ -225,6 +227,28 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
   p.glb = p.lb + nblk * 8;
   p.result = d_result;
   p.tag = c->tag;
+  if (decode_path(max_blk_len) == 2) {  // walk-scan-copy: blocks of 4 KiB .. 64 KiB - 1
+    const uint32_t cap = max_blk_len / 10 + 1;  // an entry is >= 10 B (its header)
+    const size_t meta_b = (size_t)nblk * cap * 8, tri_b = ((size_t)nblk * 24 + 255) / 256 * 256;
+    const size_t wneed = meta_b + 2 * tri_b + (size_t)nblk * 4;
+    const size_t sbytes = wsc_scan_bytes((uint32_t)nblk);
+    if (wneed > c->wsc.cap || sbytes > c->wsc_tmp.cap) {
+      HIPC(hipStreamSynchronize(c->stream));
+      HIPC(c->wsc.ensure(wneed));
+      HIPC(c->wsc_tmp.ensure(sbytes));
+    }
+    uint8_t* w = c->wsc.as<uint8_t>();
+    p.wmeta = reinterpret_cast<uint32_t*>(w);
+    p.wcap = cap;
+    p.wstat = reinterpret_cast<uint64_t*>(w + meta_b);
+    p.wbase = reinterpret_cast<uint64_t*>(w + meta_b + tri_b);
+    p.wstatus = reinterpret_cast<uint32_t*>(w + meta_b + 2 * tri_b);
+    static const uint32_t ablate =
+        getenv("LSMGPU_ABLATE") ? (uint32_t)atoi(getenv("LSMGPU_ABLATE")) : 0u;
+    p.ablate = ablate;
+    HIPC(launch_decode_wsc(p, c->wsc_tmp.p, c->wsc_tmp.cap, c->stream));
+    return LSMGPU_OK;
+  }
   uint64_t waves = 0;
   HIPC(launch_decode(p, max_blk_len, c->num_cus, c->stream, &waves));
   (void)waves;

@@ -33,6 +33,13 @@ struct DecodeParams {
   uint32_t ablate;          // timing-only diagnostics (LSMGPU_ABLATE): 1 no prefix, 2 no emit, 4 no walk
   uint32_t* census;         // residency census mode (launch_decode calibration), else nullptr
   uint64_t* stamps;         // per-phase s_memtime totals (LSMGPU_STAMPS diagnostics), else nullptr
+  // walk-scan-copy path (decode_wsc.hip): per-entry metadata (2 words x wcap per block),
+  // per-block {n, K, V} (u64 x 3), their exclusive scan, per-block status
+  uint32_t* wmeta;
+  uint32_t wcap;
+  uint64_t* wstat;
+  uint64_t* wbase;
+  uint32_t* wstatus;
 };
 
 // Encode: one wave per output block; every byte position is closed-form
@@ -67,6 +74,12 @@ struct ValuesParams {
 hipError_t launch_decode(const DecodeParams& p, uint32_t max_blk_len, int num_cus,
                          hipStream_t s, uint64_t* waves_launched);
 hipError_t launch_encode(const EncodeParams& p, int num_cus, hipStream_t s);
+// walk-scan-copy decode (blocks of 4 KiB .. 64 KiB - 1): scratch sized by the caller
+size_t wsc_scan_bytes(uint32_t nblk);
+hipError_t launch_decode_wsc(const DecodeParams& p, void* scan_tmp, size_t scan_bytes,
+                             hipStream_t s);
+// which decode path a batch takes: 0 register-lag (<= 4 KiB), 1 LDS-lag, 2 walk-scan-copy
+int decode_path(uint32_t max_blk_len);
 hipError_t launch_values_sizes(const ValuesParams& p, hipStream_t s);
 hipError_t launch_values_write(const ValuesParams& p, hipStream_t s);
 

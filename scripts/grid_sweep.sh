@@ -1,7 +1,8 @@
 #!/bin/bash
-# decode at full size with capped persistent grids: which grids run without spin timeouts
+# decode time vs persistent-grid size (workgroups per CU x 256): how latency-bound is it?
+set -o pipefail
 mkdir -p gpurun_out/probe
-for g in 256 512 640 768; do
-  LSMGPU_GRID=$g timeout -k 10 60 python bench.py --no-cpu --no-view --steps 2 --warmup 1 > gpurun_out/probe/g$g.json 2>/dev/null || exit 1
-  python -c "import json; d=json.load(open('gpurun_out/probe/g$g.json')); print('grid $g', d['roofline']['kernel_ms_mean'], d['parity'][:20])"
+for g in ${GRIDS:-1024 1536 2048 2304 2560 2816}; do
+  LSMGPU_GRID=$g timeout -k 10 60 python bench.py --no-cpu --no-view --steps 10 --warmup 2 > gpurun_out/probe/g$g.json 2>/dev/null || exit 1
+  echo "grid $g $(python scripts/bench_brief.py gpurun_out/probe/g$g.json)"
 done

@@ -15,7 +15,14 @@ import sys
 def kernel_values(path, counter):
     rows = list(csv.DictReader(open(path)))
     return [float(r["Counter_Value"]) for r in rows
-            if "decode_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter]
+            if "lsmgpu::decode" in r["Kernel_Name"] and r["Counter_Name"] == counter]
+
+
+def kernel_name(path):
+    for r in csv.DictReader(open(path)):
+        if "lsmgpu::decode" in r["Kernel_Name"]:
+            return r["Kernel_Name"].split("(")[0]
+    return "?"
 
 
 def lib_sha256():
@@ -36,7 +43,7 @@ def main():
     fetch_b = fk * 1024 * 2
     write_b = wk * 1024
     doc = {
-        "kernel": "lsmgpu::decode_kernel<4096,128,4>",
+        "kernel": kernel_name(fetch_csv),
         "mode": 1,
         "workload_bytes": int(b["config"]["workload"].split(":")[1].split("B")[0].strip()),
         "fetch_size_kib_raw": fk,

@@ -283,3 +283,31 @@ def test_many_rounds(codec, oracle, monkeypatch, grid, shape):
     _assert_same(g, oracle.decode(sst, off, ln), f"{shape} grid={grid}")
     assert g.key_data.tobytes() == cols[0].tobytes()
     assert g.val_data.tobytes() == cols[2].tobytes()
+
+
+@pytest.mark.parametrize("path", ["wsc", "lds"])
+def test_forced_decode_paths(codec, oracle, monkeypatch, path):
+    """Every decode path (LSMGPU_DECODE_PATH: walk-scan-copy, LDS-lag) on every block shape the
+    register-lag path normally takes: C2 4 KiB blocks, short entries, the KAT blocks (every
+    error status, terminators, plen > 0), prefix-compressed random blocks."""
+    monkeypatch.setenv("LSMGPU_DECODE_PATH", path)
+    c = _cols(2, 30000, seed=3)
+    sst, _, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, 0, 4096)
+    parts = [sst]
+    cols = _random_cols(20000, 5)
+    sst2, _, _ = oracle.build_cols(*cols, 0, 4096)
+    parts.append(sst2)
+    data, off, ln = _sst_blocks(oracle, parts)
+    _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln), path)
+    # KAT blocks batched at odd alignments
+    kd = bytearray()
+    offs, lens = [], []
+    for i, (_n, block, _e, _s) in enumerate(K.DECODE_KATS * 2):
+        kd += b"\xab" * (i % 13)
+        offs.append(len(kd))
+        lens.append(len(block))
+        kd += block
+    kd = bytes(kd)
+    o2, l2 = np.array(offs, np.uint32), np.array(lens, np.uint32)
+    _assert_same(codec.decode_host(kd, o2, l2), oracle.decode(kd, o2, l2), path + " kats")
+    test_prefix_compressed_random(codec, oracle)
