@@ -68,7 +68,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
       pos += klen;                                             // iterator.go:101
       if (pos + vlen > len) { st = LSMGPU_BLK_VALUE_OVERFLOW; break; }  // iterator.go:103
       pos += vlen;                                             // iterator.go:109
-      if (n < p.wcap) {
+      if (n < p.wcap && !(p.ablate & 32)) {  // (ablation 32: timing without the metadata)
         meta[2 * n] = hp | (plen << 16);
         meta[2 * n + 1] = K | (V << 16);                       // exclusive offsets (< 64 KiB)
       }
@@ -116,6 +116,32 @@ __device__ __forceinline__ void group_copy(uint8_t* dst, const uint8_t* src, uin
   }
 }
 
+// Pieces of a stream of `len` bytes (see group_copy) and piece q of it.
+__device__ __forceinline__ uint32_t n_pieces16(uint32_t len) {
+  return len >= 16 ? (len + 15) >> 4 : (len >= 4 ? 2u : len);
+}
+__device__ __forceinline__ void piece_copy(uint8_t* dst, const uint8_t* src, uint32_t len,
+                                           uint32_t q) {
+  if (len >= 16) {
+    const uint32_t o = min(16 * q, len - 16);
+    uint4 v;
+    __builtin_memcpy(&v, src + o, 16);
+    __builtin_memcpy(dst + o, &v, 16);
+  } else if (len >= 8) {
+    const uint32_t o = q ? len - 8 : 0;
+    uint2 v;
+    __builtin_memcpy(&v, src + o, 8);
+    __builtin_memcpy(dst + o, &v, 8);
+  } else if (len >= 4) {
+    const uint32_t o = q ? len - 4 : 0;
+    uint32_t v;
+    __builtin_memcpy(&v, src + o, 4);
+    __builtin_memcpy(dst + o, &v, 4);
+  } else {
+    dst[q] = src[q];
+  }
+}
+
 // K2: one wave per block, J = 8 lanes per entry.
 __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   const uint32_t lane = lane_id();
@@ -158,39 +184,69 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   if (n == 0 || (p.ablate & 2)) return;
   const uint8_t* blk = p.data + off;
   const uint32_t* meta = p.wmeta + 2ull * p.wcap * b;
-  constexpr uint32_t J = 8;
+  uint8_t* kbase = p.key_data ? p.key_data + ek : nullptr;
+  uint8_t* vbase = p.val_data ? p.val_data + ev : nullptr;
+  // J = 8 lanes per entry; an entry's pieces are [key pieces | value pieces] (16 B, the last
+  // overlapping back inside its stream, or two overlapping 8/4/2/1-B pieces below 16 B) and
+  // lane j takes pieces j, j + 8, ...  Four entry groups per pass, all loads issued first.
+  constexpr uint32_t J = 8, G = 4;
   const uint32_t j = lane & (J - 1);
-  for (uint32_t e0 = 0; e0 < n; e0 += kWave / J) {
-    const uint32_t e = e0 + (lane >> 3);
-    if (e >= n) continue;
-    const uint32_t a0 = meta[2 * e], a1 = meta[2 * e + 1];
-    const uint32_t hp = a0 & 0xffffu, plen = a0 >> 16, ko = a1 & 0xffffu, vo = a1 >> 16;
-    uint32_t ko1 = K, vo1 = V;
-    if (e + 1 < n) {
-      const uint32_t b1 = meta[2 * e + 3];
-      ko1 = b1 & 0xffffu;
-      vo1 = b1 >> 16;
-    }
-    const uint32_t kl = ko1 - ko - plen, vl = vo1 - vo;  // stored key bytes, value bytes
-    if (j == 0) {
-      if (mat) {
-        if (p.key_end) p.key_end[en + e] = (uint32_t)(ek + ko1);
-        if (p.val_end) p.val_end[en + e] = (uint32_t)(ev + vo1);
+  bool any_plen = false;
+  for (uint32_t e0 = 0; e0 < n; e0 += G * (kWave / J)) {
+    uint32_t hp[G], kl[G], vl[G], ko[G], vo[G], np[G], kp[G];
+    bool on[G];
+#pragma unroll
+    for (int i = 0; i < G; i++) {
+      const uint32_t e = e0 + i * (kWave / J) + (lane >> 3);
+      const uint32_t ec = min(e, n - 1);
+      const uint32_t a0 = meta[2 * ec], a1 = meta[2 * ec + 1];
+      const uint32_t b1 = ec + 1 < n ? meta[2 * ec + 3] : (K | (V << 16));
+      const uint32_t plen = a0 >> 16;
+      hp[i] = a0 & 0xffffu;
+      ko[i] = a1 & 0xffffu;
+      vo[i] = a1 >> 16;
+      const uint32_t ko1 = b1 & 0xffffu, vo1 = b1 >> 16;
+      kl[i] = ko1 - ko[i] - plen;  // stored key bytes
+      vl[i] = vo1 - vo[i];
+      on[i] = e < n;
+      any_plen = any_plen || (on[i] && plen != 0);
+      kp[i] = plen ? 0u : n_pieces16(kl[i]);  // prefix-compressed keys: bytewise pass below
+      np[i] = kp[i] + n_pieces16(vl[i]);
+      if (on[i] && j == 0) {
+        if (mat) {
+          if (p.key_end) p.key_end[en + e] = (uint32_t)(ek + ko1);
+          if (p.val_end) p.val_end[en + e] = (uint32_t)(ev + vo1);
+        }
+        if (view)
+          p.view[en + e] = (uint64_t)(off + hp[i] + 10) | ((uint64_t)kl[i] << 32) |
+                           ((uint64_t)vl[i] << 48);
       }
-      if (view)
-        p.view[en + e] = (uint64_t)(off + hp + 10) | ((uint64_t)kl << 32) | ((uint64_t)vl << 48);
     }
     if (!mat) continue;
-    if (p.key_data) {
-      uint8_t* kd = p.key_data + ek + ko;
-      if (plen == 0) {
-        group_copy(kd, blk + hp + 10, kl, j, J);
-      } else {  // baseKey[:plen] ++ diff (iterator.go:98-100): bytewise, rare
-        for (uint32_t i = j; i < plen + kl; i += J)
-          kd[i] = i < plen ? blk[10 + i] : blk[hp + 10 + i - plen];
+#pragma unroll
+    for (int i = 0; i < G; i++) {
+      if (!on[i]) continue;
+      for (uint32_t q = j; q < np[i]; q += J) {
+        const bool key = q < kp[i];
+        const uint32_t len = key ? kl[i] : vl[i];
+        uint8_t* dst = key ? kbase : vbase;
+        if (!dst) continue;
+        const uint32_t s0 = key ? hp[i] + 10 : hp[i] + 10 + kl[i];
+        piece_copy(dst + (key ? ko[i] : vo[i]), blk + s0, len, key ? q : q - kp[i]);
       }
     }
-    if (p.val_data) group_copy(p.val_data + ev + vo, blk + hp + 10 + kl, vl, j, J);
+  }
+  if (any_plen && kbase && mat) {  // baseKey[:plen] ++ diff (iterator.go:98-100): bytewise
+    for (uint32_t e = lane >> 3; e < n; e += kWave / J) {
+      const uint32_t a0 = meta[2 * e], a1 = meta[2 * e + 1];
+      const uint32_t plen = a0 >> 16;
+      if (plen == 0) continue;
+      const uint32_t hp = a0 & 0xffffu, ko = a1 & 0xffffu;
+      const uint32_t ko1 = e + 1 < n ? (meta[2 * e + 3] & 0xffffu) : K;
+      const uint32_t kl = ko1 - ko;
+      for (uint32_t i = j; i < kl; i += J)
+        kbase[ko + i] = i < plen ? blk[10 + i] : blk[hp + 10 + i - plen];
+    }
   }
 }
 
