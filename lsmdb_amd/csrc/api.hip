@@ -227,7 +227,7 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
   p.glb = p.lb + nblk * 8;
   p.result = d_result;
   p.tag = c->tag;
-  if (decode_path(max_blk_len) == 2) {  // walk-scan-copy: blocks of 4 KiB .. 64 KiB - 1
+  if (decode_path(max_blk_len, (uint32_t)nblk) == 2) {  // walk-scan-copy: blocks of 4 KiB .. 64 KiB - 1
     const uint32_t cap = max_blk_len / 10 + 1;  // an entry is >= 10 B (its header)
     const size_t meta_b = (size_t)nblk * cap * 8, tri_b = ((size_t)nblk * 24 + 255) / 256 * 256;
     const size_t wneed = meta_b + 2 * tri_b + (size_t)nblk * 4;

@@ -1468,19 +1468,21 @@ static hipError_t launch_cfg(const DecodeParams& p, int num_cus, hipStream_t s,
   return e;
 }
 
-int decode_path(uint32_t max_blk_len) {
+int decode_path(uint32_t max_blk_len, uint32_t nblk) {
   // LSMGPU_DECODE_PATH=reg|lds|wsc forces a path (A/B diagnostics and tests)
   const char* f = getenv("LSMGPU_DECODE_PATH");
   if (f && f[0] == 'w' && max_blk_len < 65536) return 2;
   if (f && f[0] == 'l') return 1;
   if (f && f[0] == 'r' && max_blk_len <= 4096) return 0;
-  if (max_blk_len <= 4096) return 0;
-  return max_blk_len < 65536 ? 2 : 1;  // blocks >= 64 KiB: LDS-lag kernel's global path
+  // walk-scan-copy is three launches (walk, scan, copy): it wins from ~1k blocks up; small
+  // batches stay on the single persistent kernel
+  if (max_blk_len < 65536 && nblk >= kWscMinBlocks) return 2;
+  return max_blk_len <= 4096 ? 0 : 1;
 }
 
 hipError_t launch_decode(const DecodeParams& p, uint32_t max_blk_len, int num_cus,
                          hipStream_t s, uint64_t* waves_launched) {
-  if (decode_path(max_blk_len) == 0) return launch_cfg<RegLag<128, 3>>(p, num_cus, s, waves_launched);
+  if (decode_path(max_blk_len, p.nblk) == 0) return launch_cfg<RegLag<128, 3>>(p, num_cus, s, waves_launched);
   if (max_blk_len <= 4096) return launch_cfg<LdsLag<4096, 100, 4>>(p, num_cus, s, waves_launched);
   if (max_blk_len <= 8192) return launch_cfg<LdsLag<8192, 256, 4>>(p, num_cus, s, waves_launched);
   if (max_blk_len <= 16384) return launch_cfg<LdsLag<16384, 512, 3>>(p, num_cus, s, waves_launched);

@@ -79,7 +79,9 @@ size_t wsc_scan_bytes(uint32_t nblk);
 hipError_t launch_decode_wsc(const DecodeParams& p, void* scan_tmp, size_t scan_bytes,
                              hipStream_t s);
 // which decode path a batch takes: 0 register-lag (<= 4 KiB), 1 LDS-lag, 2 walk-scan-copy
-int decode_path(uint32_t max_blk_len);
+// (blocks < 64 KiB, batches of >= kWscMinBlocks blocks)
+constexpr uint32_t kWscMinBlocks = 1024;
+int decode_path(uint32_t max_blk_len, uint32_t nblk);
 hipError_t launch_values_sizes(const ValuesParams& p, hipStream_t s);
 hipError_t launch_values_write(const ValuesParams& p, hipStream_t s);
 

@@ -261,8 +261,10 @@ def _random_cols(n, seed, kmin=9, kmax=40, vmin=3, vmax=60):
 def test_many_rounds(codec, oracle, monkeypatch, grid, shape):
     """The persistent grid capped (LSMGPU_GRID) so a modest batch runs many rounds: the
     software-pipelined emit (tile k-1 written after tile k is walked), the group look-back
-    across rounds and the LDS slot ring all get exercised, for every slot configuration."""
+    across rounds and the LDS slot ring all get exercised, for every slot configuration.
+    Large batches default to walk-scan-copy, so the persistent kernels are forced here."""
     monkeypatch.setenv("LSMGPU_GRID", str(grid))
+    monkeypatch.setenv("LSMGPU_DECODE_PATH", "reg" if shape in ("c2", "c3", "short") else "lds")
     if shape == "c2":
         c = _cols(2, 150000, seed=7)
         cols, epb, bb = (c.keys, c.key_end, c.vs, c.vs_end), 0, 4096
@@ -285,10 +287,10 @@ def test_many_rounds(codec, oracle, monkeypatch, grid, shape):
     assert g.val_data.tobytes() == cols[2].tobytes()
 
 
-@pytest.mark.parametrize("path", ["wsc", "lds"])
+@pytest.mark.parametrize("path", ["wsc", "lds", "reg"])
 def test_forced_decode_paths(codec, oracle, monkeypatch, path):
-    """Every decode path (LSMGPU_DECODE_PATH: walk-scan-copy, LDS-lag) on every block shape the
-    register-lag path normally takes: C2 4 KiB blocks, short entries, the KAT blocks (every
+    """Every decode path (LSMGPU_DECODE_PATH: walk-scan-copy, LDS-lag, register-lag) on the
+    4 KiB block shapes: C2 4 KiB blocks, short entries, the KAT blocks (every
     error status, terminators, plen > 0), prefix-compressed random blocks."""
     monkeypatch.setenv("LSMGPU_DECODE_PATH", path)
     c = _cols(2, 30000, seed=3)
