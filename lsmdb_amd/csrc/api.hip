@@ -59,6 +59,9 @@ struct lsmgpu_ctx {
   DevBuf scan_tmp;
   DevBuf wsc;            // walk-scan-copy decode scratch (metadata, per-block triples)
   DevBuf wsc_tmp;        // its scan temporary storage
+  DevBuf wsc_carry;      // chunk carries ((kWscMaxChunks + 1) x 3 u64, [0..2] = 0)
+  hipStream_t aux = nullptr;               // walk-scan-copy: the copy kernels' stream
+  hipEvent_t wev[kWscMaxChunks + 1] = {};  // chunk c walked + scanned; [chunks] copies done
   // staging for host-memory calls
   DevBuf s_data, s_off, s_len, s_kd, s_ke, s_vd, s_ve, s_view, s_bf, s_bs, s_a, s_b, s_c, s_d;
 };
@@ -106,6 +109,21 @@ int lsmgpu_open(int device, lsmgpu_ctx** out) {
     return LSMGPU_ERR_HIP;
   }
   c->stream = c->own_stream;
+  if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) {
+    lsmgpu_close(c);
+    return LSMGPU_ERR_HIP;
+  }
+  for (hipEvent_t& ev : c->wev) {
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+      lsmgpu_close(c);
+      return LSMGPU_ERR_HIP;
+    }
+  }
+  if (c->wsc_carry.ensure((kWscMaxChunks + 1) * 24) != hipSuccess ||
+      hipMemset(c->wsc_carry.p, 0, (kWscMaxChunks + 1) * 24) != hipSuccess) {
+    lsmgpu_close(c);
+    return LSMGPU_ERR_HIP;
+  }
   if (c->result.ensure(64) != hipSuccess || c->flags.ensure(64) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&c->h_result), 64, hipHostMallocDefault) != hipSuccess) {
     lsmgpu_close(c);
@@ -119,11 +137,16 @@ void lsmgpu_close(lsmgpu_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
-  DevBuf* bufs[] = {&c->lb, &c->result, &c->flags, &c->scan_tmp, &c->wsc, &c->wsc_tmp, &c->s_data,
+  if (c->aux) (void)hipStreamSynchronize(c->aux);
+  DevBuf* bufs[] = {&c->lb, &c->result, &c->flags, &c->scan_tmp, &c->wsc, &c->wsc_tmp,
+                    &c->wsc_carry, &c->s_data,
                     &c->s_off, &c->s_len, &c->s_kd, &c->s_ke, &c->s_vd, &c->s_ve, &c->s_view,
                     &c->s_bf, &c->s_bs, &c->s_a, &c->s_b, &c->s_c, &c->s_d};
   for (DevBuf* b : bufs) b->release();
   if (c->h_result) (void)hipHostFree(c->h_result);
+  for (hipEvent_t ev : c->wev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (c->aux) (void)hipStreamDestroy(c->aux);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }
@@ -227,7 +250,15 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
   p.glb = p.lb + nblk * 8;
   p.result = d_result;
   p.tag = c->tag;
-  if (decode_path(max_blk_len, (uint32_t)nblk) == 2) {  // walk-scan-copy: blocks of 4 KiB .. 64 KiB - 1
+  const int path = decode_path(max_blk_len, (uint32_t)nblk);
+  if (path == 3) {
+    static const uint32_t ablate =
+        getenv("LSMGPU_ABLATE") ? (uint32_t)atoi(getenv("LSMGPU_ABLATE")) : 0u;
+    p.ablate = ablate;
+    HIPC(launch_decode_tile(p, c->stream));
+    return LSMGPU_OK;
+  }
+  if (path == 2) {  // walk-scan-copy: blocks of 4 KiB .. 64 KiB - 1
     const uint32_t cap = max_blk_len / 10 + 1;  // an entry is >= 10 B (its header)
     const size_t meta_b = (size_t)nblk * cap * 8, tri_b = ((size_t)nblk * 24 + 255) / 256 * 256;
     const size_t wneed = meta_b + 2 * tri_b + (size_t)nblk * 4;
@@ -246,7 +277,14 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     static const uint32_t ablate =
         getenv("LSMGPU_ABLATE") ? (uint32_t)atoi(getenv("LSMGPU_ABLATE")) : 0u;
     p.ablate = ablate;
-    HIPC(launch_decode_wsc(p, c->wsc_tmp.p, c->wsc_tmp.cap, c->stream));
+    // chunks overlap one chunk's copy with the next chunk's walk (LSMGPU_WSC_CHUNKS)
+    const char* ch_env = getenv("LSMGPU_WSC_CHUNKS");
+    const int chunks = ch_env ? atoi(ch_env) : kWscChunks;
+    const int nch = nblk >= (uint64_t)chunks * kWscMinBlocks ? chunks : 1;
+    p.wb0 = 0;
+    p.wb1 = (uint32_t)nblk;
+    HIPC(launch_decode_wsc(p, c->wsc_tmp.p, c->wsc_tmp.cap, c->stream, c->aux, c->wev,
+                           c->wsc_carry.as<uint64_t>(), nch));
     return LSMGPU_OK;
   }
   uint64_t waves = 0;

@@ -20,6 +20,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include "codec_common.hpp"
+#include "decode_common.hpp"
 #include "kernels.hpp"
 
 namespace lsmgpu {
@@ -40,8 +41,8 @@ __device__ __forceinline__ void read_hdr(const uint8_t* g, uint32_t& plen, uint3
 
 // K1: lane = block.
 __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= p.nblk) return;
+  const uint32_t b = p.wb0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= p.wb1) return;
   const uint32_t off = p.blk_off[b], len = p.blk_len[b];
   uint32_t n = 0, K = 0, V = 0, st = LSMGPU_BLK_OK;
   if ((uint64_t)off + len > p.data_len) {
@@ -145,8 +146,8 @@ __device__ __forceinline__ void piece_copy(uint8_t* dst, const uint8_t* src, uin
 // K2: one wave per block, J = 8 lanes per entry.
 __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   const uint32_t lane = lane_id();
-  const uint32_t b = uniform(blockIdx.x * (blockDim.x / kWave) + (threadIdx.x >> 6));
-  if (b >= p.nblk) return;
+  const uint32_t b = uniform(p.wb0 + blockIdx.x * (blockDim.x / kWave) + (threadIdx.x >> 6));
+  if (b >= p.wb1) return;
   const uint64_t* t = p.wstat + 3ull * b;
   const uint32_t n = uniform((uint32_t)t[0]), K = uniform((uint32_t)t[1]),
                  V = uniform((uint32_t)t[2]);
@@ -250,6 +251,300 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   }
 }
 
+
+// ======================================================================= fused tile decode
+// Blocks <= 4 KiB in ONE launch that reads the input once.  A one-wave workgroup takes the
+// next tile of T consecutive blocks from an ordered ticket, LDS-DMAs them (coalesced, no
+// VGPRs), walks each block serially from LDS with one lane per block (the same chain as
+// wsc_walk_kernel, at LDS latency), publishes the tile's {entries, key bytes, value bytes},
+// finds its output base by decoupled look-back over the tile records, and copies the entries
+// global -> global as wsc_copy_kernel does (the source lines were just fetched: L2 hits).
+// The ticket gives predecessor tiles a head start, so the look-back never waits on a tile
+// that has not been scheduled.  LDS per tile: T * (4128 B slot + 410 x 8 B entry metadata).
+constexpr uint32_t kTileSlot = 4128;  // a <= 4096-B block at any 16-B shift + the tail chunk
+constexpr uint32_t kTileCap = 410;    // 409 entries of >= 10 B in 4096 B, + the sentinel
+
+template <int T>
+__global__ void __launch_bounds__(64) tile_decode_kernel(DecodeParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t slots[T * kTileSlot];
+  __shared__ uint2 meta[T * kTileCap];  // {header pos | value offset << 16, key offset}
+  const uint32_t lane = lane_id();
+  const uint32_t ntiles = (p.nblk + T - 1) / T;
+  uint32_t t = blockIdx.x;
+  if (!(p.ablate & 64)) {
+    if (lane == 0) t = atomicAdd(p.gcnt, 1u);
+    t = readlane(t, 0);
+    if (t == ntiles - 1 && lane == 0) atomicExch(p.gcnt, 0u);  // every ticket is taken
+  }
+  if (t >= ntiles) return;
+  const uint64_t tag = p.tag;
+  const uint32_t b0 = t * T;
+  const uint32_t nb = min((uint32_t)T, p.nblk - b0);
+
+  // stage the tile: block i -> slots + i * kTileSlot (16-B aligned source, shift sh)
+  // every block's [off, len) in one round trip, then all DMAs back to back
+  uint32_t lo = 0, ll = 0;
+  if (lane < nb) {
+    lo = p.blk_off[b0 + lane];
+    ll = p.blk_len[b0 + lane];
+  }
+  BlockRef ref[T];
+#pragma unroll
+  for (int i = 0; i < T; i++) {
+    ref[i] = BlockRef{0, 0, 0, false, false};
+    if ((uint32_t)i < nb)
+      ref[i] = prefetch_block<4096, 5>(p, readlane(lo, i), readlane(ll, i), slots + i * kTileSlot,
+                                       lane);
+  }
+#pragma unroll
+  for (int i = 0; i < T; i++)
+    if (ref[i].fits && ref[i].tail) land_tail(p, ref[i], slots + i * kTileSlot, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  wave_lds_fence();
+
+  // walk: lane i < nb walks block i (table/iterator.go:93-135)
+  uint32_t n = 0, K = 0, V = 0, st = LSMGPU_BLK_OK;
+  bool any_plen = false;
+  if (lane < nb && !(p.ablate & 4)) {
+    uint32_t len = 0, sh = 0;
+    bool fits = false;
+#pragma unroll
+    for (int i = 0; i < T; i++)
+      if (lane == (uint32_t)i) {
+        len = ref[i].len;
+        sh = ref[i].sh;
+        fits = ref[i].fits;
+      }
+    uint2* m = meta + lane * kTileCap;
+    if (!fits) {
+      st = LSMGPU_BLK_RANGE;  // off + len past the data (len <= 4096 on this path)
+    } else {
+      // one LDS round trip and one branch per entry: the header is read before the bounds
+      // checks (pos <= len keeps the read inside the slot), every stop condition of
+      // table/iterator.go:93-135 is evaluated at once and resolved in iterator order
+      const LdsSrc src{slots + lane * kTileSlot, sh};
+      uint32_t pos = 0;
+      for (;;) {
+        const Hdr h = src.hdr(pos);
+        const uint32_t end = pos + 10 + h.klen + h.vlen;
+        const bool eof = pos >= len;                              // iterator.go:115-118
+        const bool trunc = len - pos < 10;
+        const bool term = (h.klen | h.plen) == 0;                 // iterator.go:124-127
+        const bool fplen = n == 0 && h.plen != 0;                 // iterator.go:129-133
+        const bool poob = 10 + h.plen > len;                      // base key = entry 0's key
+        const bool vovf = end > len;                              // iterator.go:101-106
+        if (eof | trunc | term | fplen | poob | vovf) {
+          st = (eof | (!trunc & term)) ? LSMGPU_BLK_OK
+               : trunc                 ? LSMGPU_BLK_TRUNC_HEADER
+               : fplen                 ? LSMGPU_BLK_FIRST_PLEN
+               : poob                  ? LSMGPU_BLK_PREFIX_OOB
+                                       : LSMGPU_BLK_VALUE_OVERFLOW;
+          break;
+        }
+        m[n] = make_uint2(pos | (V << 16), K);
+        any_plen = any_plen || h.plen != 0;
+        K += h.plen + h.klen;
+        V += h.vlen;
+        n++;
+        pos = end;
+      }
+    }
+    m[n] = make_uint2(V << 16, K);  // sentinel: the block's key / value totals
+  }
+  wave_lds_fence();
+  const bool has_plen = __ballot(any_plen) != 0;
+
+  // tile totals, per-block exclusive offsets inside the tile, output base by look-back
+  const uint32_t in_ = wave_scan_sat(lane < nb ? n : 0u, lane);
+  const uint32_t ik = wave_scan_sat(lane < nb ? K : 0u, lane);
+  const uint32_t iv = wave_scan_sat(lane < nb ? V : 0u, lane);
+  const uint32_t nt = readlane(in_, nb - 1), kt = readlane(ik, nb - 1), vt = readlane(iv, nb - 1);
+  // Two-level prefix: every tile publishes its aggregate; the last tile of each group of 64
+  // sums the group and looks back over GROUP records (64 groups = 4096 tiles per poll), the
+  // other members add their in-group predecessors' aggregates to the previous group's
+  // inclusive prefix.  (A flat per-tile look-back advances only ~64 tiles per round trip.)
+  store3(p.lb + (uint64_t)t * 8, tag, nt, kt, vt, lane);
+  const uint32_t g = t >> 6, g0 = g << 6;
+  const uint32_t gsize = min(64u, ntiles - g0);
+  const uint32_t before = t - g0;  // in-group predecessors
+  Tot in{0, 0, 0};
+  if (before && !(p.ablate & 1)) {
+    uint32_t a = 0, b = 0, c = 0;
+    for (uint32_t spins = 0;; ++spins) {
+      bool ok = true;
+      if (lane < before) ok = read3(p.lb + (uint64_t)(g0 + lane) * 8, tag, a, b, c);
+      if (__all(ok)) break;
+      if (spins > kMaxSpins) {
+        flag_timeout(p.result, lane);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    in = Tot{wave_sum_sat(lane < before ? a : 0u), wave_sum_sat(lane < before ? b : 0u),
+             wave_sum_sat(lane < before ? c : 0u)};
+  }
+  Tot gx{0, 0, 0};  // exclusive prefix of group g
+  if (p.ablate & 1) {
+    // timing only: no prefix
+  } else if (t == g0 + gsize - 1) {  // group leader
+    const uint32_t ga = sat_add(in.n, nt), gb = sat_add(in.k, kt), gc = sat_add(in.v, vt);
+    uint64_t* Gr = p.glb + (uint64_t)g * 8;
+    if (g > 0) {
+      store3(Gr, tag, ga, gb, gc, lane);
+      gx = lookback(p.glb, g, tag, lane, p.result);
+    }
+    store3(Gr + 4, tag, sat_add(gx.n, ga), sat_add(gx.k, gb), sat_add(gx.v, gc), lane);
+  } else if (g > 0) {
+    const uint64_t* Gp = p.glb + (uint64_t)(g - 1) * 8 + 4;
+    for (uint32_t spins = 0;; ++spins) {
+      if (read3(Gp, tag, gx.n, gx.k, gx.v)) break;
+      if (spins > kMaxSpins) {
+        flag_timeout(p.result, lane);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  const Tot ex{sat_add(gx.n, in.n), sat_add(gx.k, in.k), sat_add(gx.v, in.v)};
+  const uint64_t en = ex.n, ek = ex.k, ev = ex.v;
+
+  if (lane < nb) {
+    const uint32_t b = b0 + lane;
+    if (p.blk_first) p.blk_first[b] = (uint32_t)(en + in_ - n);
+    if (p.blk_status) p.blk_status[b] = (int32_t)st;
+    if (st != LSMGPU_BLK_OK) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(p.result + 4), 1ull);
+      atomicMax(reinterpret_cast<unsigned long long*>(p.result + 3),
+                (unsigned long long)(p.nblk - b));
+    }
+  }
+  if (t == ntiles - 1 && lane == 0) {  // totals of the whole batch
+    if (p.blk_first) p.blk_first[p.nblk] = (uint32_t)(en + nt);
+    p.result[0] = en + nt;
+    p.result[1] = ek + kt;
+    p.result[2] = ev + vt;
+  }
+  const bool mat = (p.mode & LSMGPU_MODE_MATERIALIZE) != 0;
+  const bool view = (p.mode & LSMGPU_MODE_VIEW) != 0 && p.view;
+  bool ok = en + nt <= p.ent_cap && en + nt <= 0xffffffffull;
+  if (mat) {
+    const uint64_t kend = ek + kt, vend = ev + vt;
+    ok = ok && (kend <= p.key_cap || !p.key_data) && (vend <= p.val_cap || !p.val_data);
+    ok = ok && kend < 0xffffffffull && vend <= 0xffffffffull;
+  }
+  if (!ok) {
+    if (lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(p.result + 5), 1ull);
+    return;
+  }
+  if (nt == 0 || (p.ablate & 2)) return;
+
+  // per-block constants of the tile (uniform): first entry, key / value offsets, source
+  uint32_t fb[T], kb[T], vb[T], bo[T], bsh[T];
+#pragma unroll
+  for (int i = 0; i < T; i++) {
+    fb[i] = (uint32_t)i < nb ? readlane(in_ - n, i) : 0xffffffffu;
+    kb[i] = readlane(ik - K, i);
+    vb[i] = readlane(iv - V, i);
+    bo[i] = ref[i].off;
+    bsh[i] = ref[i].sh;
+  }
+  uint8_t* kbase = p.key_data ? p.key_data + ek : nullptr;
+  uint8_t* vbase = p.val_data ? p.val_data + ev : nullptr;
+  constexpr uint32_t J = 8, G = 4;
+  const uint32_t j = lane & (J - 1);
+  for (uint32_t e0 = 0; e0 < nt; e0 += G * (kWave / J)) {
+    uint32_t kl[G], ks[G], vl[G], ko[G], vo[G], np[G], kp[G], src[G];
+    bool on[G];
+#pragma unroll
+    for (int i = 0; i < G; i++) {
+      const uint32_t e = e0 + i * (kWave / J) + (lane >> 3);
+      const uint32_t ec = min(e, nt - 1);
+      uint32_t blk = 0;
+#pragma unroll
+      for (int q = 1; q < T; q++) blk += ec >= fb[q] ? 1u : 0u;
+      uint32_t f = fb[0], kx = kb[0], vx = vb[0], o = bo[0], shb = bsh[0];
+#pragma unroll
+      for (int q = 1; q < T; q++)
+        if (blk == (uint32_t)q) {
+          f = fb[q];
+          kx = kb[q];
+          vx = vb[q];
+          o = bo[q];
+          shb = bsh[q];
+        }
+      const uint2 m0 = meta[blk * kTileCap + ec - f], m1 = meta[blk * kTileCap + ec - f + 1];
+      const uint32_t hp = m0.x & 0xffffu;
+      vo[i] = vx + (m0.x >> 16);
+      ko[i] = kx + m0.y;
+      kl[i] = m1.y - m0.y;  // output key bytes (plen + stored)
+      vl[i] = (m1.x >> 16) - (m0.x >> 16);
+      src[i] = o + hp + 10;
+      // stored key bytes: the output key less its shared prefix (prefix-compressed tiles only)
+      ks[i] = has_plen ? kl[i] - LdsSrc{slots + blk * kTileSlot, shb}.hdr(hp).plen : kl[i];
+      on[i] = e < nt;
+      kp[i] = has_plen ? 0u : n_pieces16(kl[i]);  // prefix-compressed tiles: bytewise below
+      np[i] = kp[i] + n_pieces16(vl[i]);
+      if (on[i] && j == 0) {
+        if (mat) {
+          if (p.key_end) p.key_end[en + e] = (uint32_t)(ek + ko[i] + kl[i]);
+          if (p.val_end) p.val_end[en + e] = (uint32_t)(ev + vo[i] + vl[i]);
+        }
+        if (view)
+          p.view[en + e] = (uint64_t)src[i] | ((uint64_t)ks[i] << 32) | ((uint64_t)vl[i] << 48);
+      }
+    }
+    if (!mat) continue;
+#pragma unroll
+    for (int i = 0; i < G; i++) {
+      if (!on[i]) continue;
+      for (uint32_t q = j; q < np[i]; q += J) {
+        const bool key = q < kp[i];
+        uint8_t* dst = key ? kbase : vbase;
+        if (!dst) continue;
+        const uint32_t len = key ? kl[i] : vl[i];
+        piece_copy(dst + (key ? ko[i] : vo[i]), p.data + (key ? src[i] : src[i] + ks[i]), len,
+                   key ? q : q - kp[i]);
+      }
+    }
+  }
+  if (has_plen && kbase && mat) {  // baseKey[:plen] ++ diff (iterator.go:98-100): bytewise
+    for (uint32_t e = lane >> 3; e < nt; e += kWave / J) {
+      uint32_t blk = 0;
+#pragma unroll
+      for (int q = 1; q < T; q++) blk += e >= fb[q] ? 1u : 0u;
+      uint32_t f = fb[0], kx = kb[0], o = bo[0], shb = bsh[0];
+#pragma unroll
+      for (int q = 1; q < T; q++)
+        if (blk == (uint32_t)q) {
+          f = fb[q];
+          kx = kb[q];
+          o = bo[q];
+          shb = bsh[q];
+        }
+      const uint2 m0 = meta[blk * kTileCap + e - f], m1 = meta[blk * kTileCap + e - f + 1];
+      const uint32_t hp = m0.x & 0xffffu;
+      const uint32_t plen = LdsSrc{slots + blk * kTileSlot, shb}.hdr(hp).plen;
+      const uint32_t kl = m1.y - m0.y;
+      const uint8_t* blk_p = p.data + o;
+      for (uint32_t i = j; i < kl; i += J)
+        kbase[kx + m0.y + i] = i < plen ? blk_p[10 + i] : blk_p[hp + 10 + i - plen];
+    }
+  }
+}
+
+hipError_t launch_decode_tile(const DecodeParams& p, hipStream_t s) {
+  static const int T = getenv("LSMGPU_TILE") ? atoi(getenv("LSMGPU_TILE")) : 2;
+  const uint32_t nblk = p.nblk;
+  if (T == 1) {
+    hipLaunchKernelGGL(tile_decode_kernel<1>, dim3(nblk), dim3(64), 0, s, p);
+  } else if (T == 4) {
+    hipLaunchKernelGGL(tile_decode_kernel<4>, dim3((nblk + 3) / 4), dim3(64), 0, s, p);
+  } else {
+    hipLaunchKernelGGL(tile_decode_kernel<2>, dim3((nblk + 1) / 2), dim3(64), 0, s, p);
+  }
+  return hipGetLastError();
+}
+
 namespace {
 struct Tri64 {
   uint64_t n, k, v;
@@ -261,26 +556,59 @@ struct Tri64Plus {
 };
 }  // namespace
 
+// chunk c's scan starts from carry[c] = the inclusive totals of every earlier chunk
+__global__ void wsc_carry_kernel(const uint64_t* wstat, const uint64_t* wbase, uint32_t last,
+                                 uint64_t* carry) {
+  if (threadIdx.x < 3) carry[threadIdx.x] = wbase[3ull * last + threadIdx.x] + wstat[3ull * last + threadIdx.x];
+}
+
 size_t wsc_scan_bytes(uint32_t nblk) {
   size_t bytes = 0;
   (void)rocprim::exclusive_scan(nullptr, bytes, (const Tri64*)nullptr, (Tri64*)nullptr,
-                                Tri64{0, 0, 0}, (size_t)nblk, Tri64Plus());
+                                rocprim::future_value<Tri64>(nullptr), (size_t)nblk, Tri64Plus());
   return bytes;
 }
 
 hipError_t launch_decode_wsc(const DecodeParams& p, void* scan_tmp, size_t scan_bytes,
-                             hipStream_t s) {
+                             hipStream_t s, hipStream_t aux, hipEvent_t* ev, uint64_t* carry,
+                             int chunks) {
   const uint32_t nblk = p.nblk;
-  hipLaunchKernelGGL(wsc_walk_kernel, dim3((nblk + 255) / 256), dim3(256), 0, s, p);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  size_t bytes = scan_bytes;
-  e = rocprim::exclusive_scan(scan_tmp, bytes, reinterpret_cast<const Tri64*>(p.wstat),
-                              reinterpret_cast<Tri64*>(p.wbase), Tri64{0, 0, 0}, (size_t)nblk,
-                              Tri64Plus(), s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(wsc_copy_kernel, dim3((nblk + 3) / 4), dim3(256), 0, s, p);
-  return hipGetLastError();
+  if (chunks < 1 || !aux) chunks = 1;
+  if (chunks > kWscMaxChunks) chunks = kWscMaxChunks;
+  if ((uint32_t)chunks > nblk) chunks = (int)nblk;
+  hipError_t e = hipSuccess;
+  for (int c = 0; c < chunks; c++) {
+    DecodeParams q = p;
+    q.wb0 = (uint32_t)((uint64_t)nblk * c / chunks);
+    q.wb1 = (uint32_t)((uint64_t)nblk * (c + 1) / chunks);
+    const uint32_t nb = q.wb1 - q.wb0;
+    hipLaunchKernelGGL(wsc_walk_kernel, dim3((nb + 255) / 256), dim3(256), 0, s, q);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    size_t bytes = scan_bytes;
+    e = rocprim::exclusive_scan(scan_tmp, bytes, reinterpret_cast<const Tri64*>(p.wstat + 3ull * q.wb0),
+                                reinterpret_cast<Tri64*>(p.wbase + 3ull * q.wb0),
+                                rocprim::future_value<Tri64>(reinterpret_cast<Tri64*>(carry + 3 * c)),
+                                (size_t)nb, Tri64Plus(), s);
+    if (e != hipSuccess) return e;
+    if (c + 1 < chunks) {
+      hipLaunchKernelGGL(wsc_carry_kernel, dim3(1), dim3(64), 0, s, p.wstat, p.wbase, q.wb1 - 1,
+                         carry + 3 * (c + 1));
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    hipStream_t cs = s;
+    if (chunks > 1) {
+      if ((e = hipEventRecord(ev[c], s)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(aux, ev[c], 0)) != hipSuccess) return e;
+      cs = aux;
+    }
+    hipLaunchKernelGGL(wsc_copy_kernel, dim3((nb + 3) / 4), dim3(256), 0, cs, q);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if (chunks > 1) {
+    if ((e = hipEventRecord(ev[chunks], aux)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(s, ev[chunks], 0)) != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace lsmgpu

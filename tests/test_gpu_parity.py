@@ -287,9 +287,9 @@ def test_many_rounds(codec, oracle, monkeypatch, grid, shape):
     assert g.val_data.tobytes() == cols[2].tobytes()
 
 
-@pytest.mark.parametrize("path", ["wsc", "lds", "reg"])
+@pytest.mark.parametrize("path", ["wsc", "lds", "reg", "tile"])
 def test_forced_decode_paths(codec, oracle, monkeypatch, path):
-    """Every decode path (LSMGPU_DECODE_PATH: walk-scan-copy, LDS-lag, register-lag) on the
+    """Every decode path (LSMGPU_DECODE_PATH: walk-scan-copy, LDS-lag, register-lag, fused tile) on the
     4 KiB block shapes: C2 4 KiB blocks, short entries, the KAT blocks (every
     error status, terminators, plen > 0), prefix-compressed random blocks."""
     monkeypatch.setenv("LSMGPU_DECODE_PATH", path)
@@ -313,3 +313,21 @@ def test_forced_decode_paths(codec, oracle, monkeypatch, path):
     o2, l2 = np.array(offs, np.uint32), np.array(lens, np.uint32)
     _assert_same(codec.decode_host(kd, o2, l2), oracle.decode(kd, o2, l2), path + " kats")
     test_prefix_compressed_random(codec, oracle)
+
+
+@pytest.mark.parametrize("chunks", [2, 3, 8])
+def test_wsc_chunked(codec, oracle, monkeypatch, chunks):
+    """Walk-scan-copy split into block-range chunks: chunk c's copy runs on the auxiliary stream
+    while chunk c+1 is walked; each chunk's scan starts from the device-side carry of the
+    chunks before it.  Ragged chunk boundaries (nblk not a multiple of the chunk count)."""
+    monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
+    monkeypatch.setenv("LSMGPU_WSC_CHUNKS", str(chunks))
+    c = _cols(2, 34 * 1024 * chunks + 777, seed=21)
+    sst, _, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, 0, 4096)
+    sst = sst + b"{}" + (2).to_bytes(4, "big")
+    off, ln, _, _ = oracle.parse_index(sst)
+    assert len(off) >= 1024 * chunks
+    g = codec.decode_host(sst, off, ln)
+    _assert_same(g, oracle.decode(sst, off, ln), f"chunks={chunks}")
+    assert g.key_data.tobytes() == c.keys.tobytes()
+    assert g.val_data.tobytes() == c.vs.tobytes()
