@@ -283,6 +283,11 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     const int nch = nblk >= (uint64_t)chunks * kWscMinBlocks ? chunks : 1;
     p.wb0 = 0;
     p.wb1 = (uint32_t)nblk;
+    // big blocks: several waves copy one block (more bytes in flight per block); LSMGPU_WSC_SPLIT
+    const char* sp_env = getenv("LSMGPU_WSC_SPLIT");
+    uint32_t split = max_blk_len > 8192 ? 2u : 1u;  // measured: C5 1.25 -> 1.09 ms at 2
+    if (sp_env) split = (uint32_t)atoi(sp_env);
+    p.wsplit = (split == 2 || split == 4) ? split : 1u;
     HIPC(launch_decode_wsc(p, c->wsc_tmp.p, c->wsc_tmp.cap, c->stream, c->aux, c->wev,
                            c->wsc_carry.as<uint64_t>(), nch));
     return LSMGPU_OK;

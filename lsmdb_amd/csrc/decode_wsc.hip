@@ -146,7 +146,10 @@ __device__ __forceinline__ void piece_copy(uint8_t* dst, const uint8_t* src, uin
 // K2: one wave per block, J = 8 lanes per entry.
 __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   const uint32_t lane = lane_id();
-  const uint32_t b = uniform(p.wb0 + blockIdx.x * (blockDim.x / kWave) + (threadIdx.x >> 6));
+  // p.wsplit waves share a block (large blocks): wave `sub` takes passes sub, sub + wsplit, ...
+  const uint32_t wave = threadIdx.x >> 6, split = p.wsplit;
+  const uint32_t sub = wave % split;
+  const uint32_t b = uniform(p.wb0 + blockIdx.x * (blockDim.x / kWave / split) + wave / split);
   if (b >= p.wb1) return;
   const uint64_t* t = p.wstat + 3ull * b;
   const uint32_t n = uniform((uint32_t)t[0]), K = uniform((uint32_t)t[1]),
@@ -155,7 +158,7 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   const uint64_t* bs = p.wbase + 3ull * b;
   const uint64_t en = uniform64(bs[0]), ek = uniform64(bs[1]), ev = uniform64(bs[2]);
   const uint32_t off = uniform(p.blk_off[b]);
-  if (lane == 0) {
+  if (lane == 0 && sub == 0) {
     if (p.blk_first) p.blk_first[b] = (uint32_t)en;
     if (p.blk_status) p.blk_status[b] = (int32_t)st;
     if (st != LSMGPU_BLK_OK) {
@@ -179,7 +182,7 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
     ok = ok && kend < 0xffffffffull && vend <= 0xffffffffull;
   }
   if (!ok) {
-    if (lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(p.result + 5), 1ull);
+    if (lane == 0 && sub == 0) atomicOr(reinterpret_cast<unsigned long long*>(p.result + 5), 1ull);
     return;
   }
   if (n == 0 || (p.ablate & 2)) return;
@@ -193,7 +196,7 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   constexpr uint32_t J = 8, G = 4;
   const uint32_t j = lane & (J - 1);
   bool any_plen = false;
-  for (uint32_t e0 = 0; e0 < n; e0 += G * (kWave / J)) {
+  for (uint32_t e0 = sub * G * (kWave / J); e0 < n; e0 += split * G * (kWave / J)) {
     uint32_t hp[G], kl[G], vl[G], ko[G], vo[G], np[G], kp[G];
     bool on[G];
 #pragma unroll
@@ -238,7 +241,10 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
     }
   }
   if (any_plen && kbase && mat) {  // baseKey[:plen] ++ diff (iterator.go:98-100): bytewise
-    for (uint32_t e = lane >> 3; e < n; e += kWave / J) {
+    // the same passes as above (any_plen covers only this wave's entries)
+    for (uint32_t e = sub * G * (kWave / J) + (lane >> 3); e < n;
+         e += ((e / (kWave / J)) % G == G - 1) ? (split - 1) * G * (kWave / J) + kWave / J
+                                              : kWave / J) {
       const uint32_t a0 = meta[2 * e], a1 = meta[2 * e + 1];
       const uint32_t plen = a0 >> 16;
       if (plen == 0) continue;
@@ -601,7 +607,8 @@ hipError_t launch_decode_wsc(const DecodeParams& p, void* scan_tmp, size_t scan_
       if ((e = hipStreamWaitEvent(aux, ev[c], 0)) != hipSuccess) return e;
       cs = aux;
     }
-    hipLaunchKernelGGL(wsc_copy_kernel, dim3((nb + 3) / 4), dim3(256), 0, cs, q);
+    const uint32_t per_wg = 4 / q.wsplit;  // blocks per 4-wave workgroup
+    hipLaunchKernelGGL(wsc_copy_kernel, dim3((nb + per_wg - 1) / per_wg), dim3(256), 0, cs, q);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   if (chunks > 1) {

@@ -41,6 +41,7 @@ struct DecodeParams {
   uint64_t* wbase;
   uint32_t* wstatus;
   uint32_t wb0, wb1;        // walk-scan-copy: this launch's block range [wb0, wb1)
+  uint32_t wsplit;          // walk-scan-copy: waves per block in the copy (1, 2 or 4)
 };
 
 // Encode: one wave per output block; every byte position is closed-form

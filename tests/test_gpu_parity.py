@@ -331,3 +331,18 @@ def test_wsc_chunked(codec, oracle, monkeypatch, chunks):
     _assert_same(g, oracle.decode(sst, off, ln), f"chunks={chunks}")
     assert g.key_data.tobytes() == c.keys.tobytes()
     assert g.val_data.tobytes() == c.vs.tobytes()
+
+
+@pytest.mark.parametrize("split", [1, 2, 4])
+def test_wsc_split(codec, oracle, monkeypatch, split):
+    """Walk-scan-copy with 1, 2 or 4 waves sharing each block's copy (LSMGPU_WSC_SPLIT): C5
+    Zipf-key 32 KiB blocks, prefix-compressed random blocks, short-entry 4 KiB blocks."""
+    monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
+    monkeypatch.setenv("LSMGPU_WSC_SPLIT", str(split))
+    c = _cols(5, 60000, seed=9)
+    sst, _, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, c.entries_per_block,
+                                  c.block_bytes)
+    parts = [sst, oracle.build_cols(*_random_cols(30000, 4), 0, 4096)[0]]
+    data, off, ln = _sst_blocks(oracle, parts)
+    _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln), f"split={split}")
+    test_prefix_compressed_random(codec, oracle)
