@@ -259,8 +259,10 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     return LSMGPU_OK;
   }
   if (path == 2) {  // walk-scan-copy: blocks of 4 KiB .. 64 KiB - 1
-    const uint32_t cap = max_blk_len / 10 + 1;  // an entry is >= 10 B (its header)
-    const size_t meta_b = (size_t)nblk * cap * 8, tri_b = ((size_t)nblk * 24 + 255) / 256 * 256;
+    // entries of a block (>= 10 B each) + the sentinel, rounded to 16-entry (128-B) chunks
+    const uint32_t cap = (max_blk_len / 10 + 1 + 15) / 16 * 16;
+    const size_t meta_b = (size_t)nblk * cap * 8;
+    const size_t tri_b = ((size_t)nblk * 24 + 255) / 256 * 256;
     const size_t wneed = meta_b + 2 * tri_b + (size_t)nblk * 4;
     const size_t sbytes = wsc_scan_bytes((uint32_t)nblk);
     if (wneed > c->wsc.cap || sbytes > c->wsc_tmp.cap) {
@@ -288,7 +290,9 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     uint32_t split = max_blk_len > 8192 ? 2u : 1u;  // measured: C5 1.25 -> 1.09 ms at 2
     if (sp_env) split = (uint32_t)atoi(sp_env);
     p.wsplit = (split == 2 || split == 4) ? split : 1u;
-    HIPC(launch_decode_wsc(p, c->wsc_tmp.p, c->wsc_tmp.cap, c->stream, c->aux, c->wev,
+    const bool one_stream = getenv("LSMGPU_WSC_ONE_STREAM") != nullptr;
+    HIPC(launch_decode_wsc(p, c->wsc_tmp.p, c->wsc_tmp.cap, c->stream,
+                           one_stream ? nullptr : c->aux, c->wev,
                            c->wsc_carry.as<uint64_t>(), nch));
     return LSMGPU_OK;
   }

@@ -211,11 +211,11 @@ __device__ void group_lead(const DecodeParams& p, uint32_t b, uint64_t tag, uint
   const uint32_t g0 = g << 6;
   const uint32_t gsize = (p.nblk - g0 < 64u) ? (p.nblk - g0) : 64u;
   uint32_t a = 0, bk = 0, c = 0;
-  for (uint32_t spins = 0;; ++spins) {
+  for (SpinBound bound;;) {
     bool ok = true;
     if (lane < gsize) ok = read3(p.lb + (uint64_t)(g0 + lane) * 8, tag, a, bk, c);
     if (__all(ok)) break;
-    if (spins > kMaxSpins) {
+    if (bound.expired()) {
       flag_timeout(p.result, lane);
       break;
     }
@@ -248,13 +248,13 @@ __device__ void group_lead(const DecodeParams& p, uint32_t b, uint64_t tag, uint
 __device__ __forceinline__ Tot prefix_of(const DecodeParams& p, uint32_t b, uint64_t x,
                                          uint64_t tag, uint32_t lane) {
   const uint64_t* X = p.lb + (uint64_t)b * 8 + 4;
-  for (uint32_t spins = 0;; ++spins) {
+  for (SpinBound bound;;) {
     const bool ok = lane >= 3 || (x >> kTagShift) == tag;
     if (__all(ok)) {
       const uint32_t v = (uint32_t)x;
       return Tot{readlane(v, 0), readlane(v, 1), readlane(v, 2)};
     }
-    if (spins > kMaxSpins) {
+    if (bound.expired()) {
       flag_timeout(p.result, lane);
       return Tot{0, 0, 0};
     }

@@ -81,7 +81,20 @@ struct Tot {
   uint32_t n, k, v;
 };
 
-constexpr uint32_t kMaxSpins = 1u << 16;  // ~4 ms of polling: a hard bound, never expected
+// Poll bound: wall-clock, not a poll count -- a legal but slow predecessor (a block of
+// thousands of prefix-compressed entries with megabytes of output keys) may take milliseconds;
+// only a real deadlock runs into the bound, which then ends the wait with an error flag.
+constexpr uint64_t kSpinTimeoutTicks = 200000000ull;  // 2 s of the 100 MHz s_memrealtime clock
+struct SpinBound {
+  uint64_t t0 = 0;
+  uint32_t polls = 0;
+  __device__ __forceinline__ bool expired() {  // call once per unsuccessful poll
+    if ((++polls & 255u) != 0) return false;   // read the clock every 256 polls
+    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    if (t0 == 0) t0 = t;
+    return t - t0 > kSpinTimeoutTicks;
+  }
+};
 
 __device__ __forceinline__ void flag_timeout(uint64_t* result, uint32_t lane) {
   if (lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(result + 5), 2ull);
@@ -129,7 +142,7 @@ __device__ inline Tot lookback(const uint64_t* rec, uint32_t g, uint64_t tag, ui
   Tot ex{0, 0, 0};
   int64_t j0 = (int64_t)g - 1;
   uint32_t wsize = 8;
-  uint32_t spins = 0;
+  SpinBound bound;
   while (j0 >= 0) {
     const int64_t j = j0 - (int64_t)lane;
     bool inc = false, ready = false;
@@ -149,7 +162,7 @@ __device__ inline Tot lookback(const uint64_t* rec, uint32_t g, uint64_t tag, ui
     const uint32_t last = first < wsize ? first : wsize - 1;
     const uint64_t need = (last >= 63) ? ~0ull : ((1ull << (last + 1)) - 1);
     if ((rm & need) != need) {
-      if (++spins > kMaxSpins) {
+      if (bound.expired()) {
         flag_timeout(result, lane);
         return ex;
       }

@@ -8,9 +8,9 @@
 // flight, each hop one dependent 8-B load -- and the bytes are then moved by a separate,
 // fully parallel copy with known output bases:
 //   K1 walk_kernel : lane b walks block b exactly like blockIterator.Next/parseKV
-//                    (table/iterator.go:93-135), writing per entry {pos | plen << 16,
-//                    key offset | value offset << 16} into the block's metadata region and
-//                    {entries, key bytes, value bytes} + status per block
+//                    (table/iterator.go:93-135), writing per entry {pos | value offset << 16,
+//                    key offset} (full-line chunks, see flush_meta) and {entries, key
+//                    bytes, value bytes} + status per block
 //   scan           : rocPRIM exclusive scan of the per-block triples (device-wide)
 //   K2 copy_kernel : one wave per block; lane groups copy each entry's key and value as
 //                    unaligned 16-B pieces (the last overlapping back inside the entry, so
@@ -39,45 +39,63 @@ __device__ __forceinline__ void read_hdr(const uint8_t* g, uint32_t& plen, uint3
 
 }  // namespace
 
+// Per-entry metadata of the walk: uint2 {header pos | value offset << 16, key offset} (key
+// offsets count plen + stored bytes: u32, prefix-compressed blocks may pass 64 KiB), entry n
+// = the sentinel {stop pos | V << 16, K}.  Block b's entries are contiguous at b * wcap
+// (wcap a multiple of 16: 128-B aligned chunks of 16 entries).  The walking lane stages 16
+// entries in LDS and writes each chunk as one full 128-B line -- 8-B stores straight from
+// 64 lanes at 64 different blocks were evicted from L2 as partial lines (4x the bytes).
+constexpr uint32_t kWalkStage = 17;  // uint2 per lane row: 16 entries + 1 pad (bank spread)
+
+__device__ __forceinline__ void flush_meta(uint2* dst, const uint2* row, uint32_t cnt) {
+  if (cnt == 16) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      uint4 v;
+      v.x = row[2 * i].x;
+      v.y = row[2 * i].y;
+      v.z = row[2 * i + 1].x;
+      v.w = row[2 * i + 1].y;
+      reinterpret_cast<uint4*>(dst)[i] = v;
+    }
+  } else {
+    for (uint32_t i = 0; i < cnt; i++) dst[i] = row[i];
+  }
+}
+
 // K1: lane = block.
 __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
+  __shared__ uint2 stage[256 * kWalkStage];
+  uint2* row = stage + threadIdx.x * kWalkStage;
   const uint32_t b = p.wb0 + blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= p.wb1) return;
   const uint32_t off = p.blk_off[b], len = p.blk_len[b];
-  uint32_t n = 0, K = 0, V = 0, st = LSMGPU_BLK_OK;
+  uint32_t n = 0, K = 0, V = 0, st = LSMGPU_BLK_OK, pos = 0;
+  uint2* meta = reinterpret_cast<uint2*>(p.wmeta) + (uint64_t)b * p.wcap;
   if ((uint64_t)off + len > p.data_len) {
     st = LSMGPU_BLK_RANGE;
   } else {
     const uint8_t* blk = p.data + off;
-    uint32_t* meta = p.wmeta + 2ull * p.wcap * b;
-    uint32_t pos = 0, base_pos = 0;
-    bool have_base = false;
     for (;;) {
       if (pos >= len) break;                                   // iterator.go:115-118
       if (len - pos < 10) { st = LSMGPU_BLK_TRUNC_HEADER; break; }
       uint32_t plen, klen, vlen;
-      read_hdr(blk + pos, plen, klen, vlen);
-      const uint32_t hp = pos;
-      pos += 10;                                               // iterator.go:121
+      read_hdr(blk + pos, plen, klen, vlen);                   // iterator.go:121
       if ((klen | plen) == 0) break;                           // iterator.go:124-127
-      if (!have_base) {                                        // iterator.go:129-133
-        if (plen != 0) { st = LSMGPU_BLK_FIRST_PLEN; break; }
-        base_pos = pos;
-        have_base = true;
-      }
-      if (base_pos + plen > len) { st = LSMGPU_BLK_PREFIX_OOB; break; }
-      pos += klen;                                             // iterator.go:101
-      if (pos + vlen > len) { st = LSMGPU_BLK_VALUE_OVERFLOW; break; }  // iterator.go:103
-      pos += vlen;                                             // iterator.go:109
-      if (n < p.wcap && !(p.ablate & 32)) {  // (ablation 32: timing without the metadata)
-        meta[2 * n] = hp | (plen << 16);
-        meta[2 * n + 1] = K | (V << 16);                       // exclusive offsets (< 64 KiB)
-      }
+      if (n == 0 && plen != 0) { st = LSMGPU_BLK_FIRST_PLEN; break; }  // iterator.go:129-133
+      if (10 + plen > len) { st = LSMGPU_BLK_PREFIX_OOB; break; }      // base key = entry 0's
+      const uint32_t end = pos + 10 + klen + vlen;             // iterator.go:101-109
+      if (end > len) { st = LSMGPU_BLK_VALUE_OVERFLOW; break; }
+      row[n & 15] = make_uint2(pos | (V << 16), K);  // n < wcap - 1: >= 10 B per entry
+      if ((n & 15) == 15) flush_meta(meta + (n - 15), row, 16);
       K += plen + klen;
       V += vlen;
       n++;
+      pos = end;
     }
   }
+  row[n & 15] = make_uint2(pos | (V << 16), K);
+  flush_meta(meta + (n & ~15u), row, (n & 15) + 1);
   uint64_t* t = p.wstat + 3ull * b;
   t[0] = n;
   t[1] = K;
@@ -149,7 +167,7 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   // p.wsplit waves share a block (large blocks): wave `sub` takes passes sub, sub + wsplit, ...
   const uint32_t wave = threadIdx.x >> 6, split = p.wsplit;
   const uint32_t sub = wave % split;
-  const uint32_t b = uniform(p.wb0 + blockIdx.x * (blockDim.x / kWave / split) + wave / split);
+  const uint32_t b = uniform(p.wb0 + blockIdx.x * (4 / split) + wave / split);
   if (b >= p.wb1) return;
   const uint64_t* t = p.wstat + 3ull * b;
   const uint32_t n = uniform((uint32_t)t[0]), K = uniform((uint32_t)t[1]),
@@ -187,7 +205,7 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   }
   if (n == 0 || (p.ablate & 2)) return;
   const uint8_t* blk = p.data + off;
-  const uint32_t* meta = p.wmeta + 2ull * p.wcap * b;
+  const uint2* meta = reinterpret_cast<const uint2*>(p.wmeta) + (uint64_t)b * p.wcap;
   uint8_t* kbase = p.key_data ? p.key_data + ek : nullptr;
   uint8_t* vbase = p.val_data ? p.val_data + ev : nullptr;
   // J = 8 lanes per entry; an entry's pieces are [key pieces | value pieces] (16 B, the last
@@ -203,15 +221,14 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
     for (int i = 0; i < G; i++) {
       const uint32_t e = e0 + i * (kWave / J) + (lane >> 3);
       const uint32_t ec = min(e, n - 1);
-      const uint32_t a0 = meta[2 * ec], a1 = meta[2 * ec + 1];
-      const uint32_t b1 = ec + 1 < n ? meta[2 * ec + 3] : (K | (V << 16));
-      const uint32_t plen = a0 >> 16;
-      hp[i] = a0 & 0xffffu;
-      ko[i] = a1 & 0xffffu;
-      vo[i] = a1 >> 16;
-      const uint32_t ko1 = b1 & 0xffffu, vo1 = b1 >> 16;
-      kl[i] = ko1 - ko[i] - plen;  // stored key bytes
+      const uint2 m0 = meta[ec], m1 = meta[ec + 1];
+      hp[i] = m0.x & 0xffffu;
+      vo[i] = m0.x >> 16;
+      ko[i] = m0.y;
+      const uint32_t ko1 = m1.y, vo1 = m1.x >> 16;
       vl[i] = vo1 - vo[i];
+      kl[i] = (m1.x & 0xffffu) - hp[i] - 10 - vl[i];  // stored key bytes
+      const uint32_t plen = ko1 - ko[i] - kl[i];
       on[i] = e < n;
       any_plen = any_plen || (on[i] && plen != 0);
       kp[i] = plen ? 0u : n_pieces16(kl[i]);  // prefix-compressed keys: bytewise pass below
@@ -245,12 +262,12 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
     for (uint32_t e = sub * G * (kWave / J) + (lane >> 3); e < n;
          e += ((e / (kWave / J)) % G == G - 1) ? (split - 1) * G * (kWave / J) + kWave / J
                                               : kWave / J) {
-      const uint32_t a0 = meta[2 * e], a1 = meta[2 * e + 1];
-      const uint32_t plen = a0 >> 16;
+      const uint2 m0 = meta[e], m1 = meta[e + 1];
+      const uint32_t hp = m0.x & 0xffffu, ko = m0.y;
+      const uint32_t vl = (m1.x >> 16) - (m0.x >> 16);
+      const uint32_t kl = m1.y - ko;                                // output key bytes
+      const uint32_t plen = kl - ((m1.x & 0xffffu) - hp - 10 - vl);
       if (plen == 0) continue;
-      const uint32_t hp = a0 & 0xffffu, ko = a1 & 0xffffu;
-      const uint32_t ko1 = e + 1 < n ? (meta[2 * e + 3] & 0xffffu) : K;
-      const uint32_t kl = ko1 - ko;
       for (uint32_t i = j; i < kl; i += J)
         kbase[ko + i] = i < plen ? blk[10 + i] : blk[hp + 10 + i - plen];
     }
@@ -376,11 +393,11 @@ __global__ void __launch_bounds__(64) tile_decode_kernel(DecodeParams p) {
   Tot in{0, 0, 0};
   if (before && !(p.ablate & 1)) {
     uint32_t a = 0, b = 0, c = 0;
-    for (uint32_t spins = 0;; ++spins) {
+    for (SpinBound bound;;) {
       bool ok = true;
       if (lane < before) ok = read3(p.lb + (uint64_t)(g0 + lane) * 8, tag, a, b, c);
       if (__all(ok)) break;
-      if (spins > kMaxSpins) {
+      if (bound.expired()) {
         flag_timeout(p.result, lane);
         break;
       }
@@ -402,9 +419,9 @@ __global__ void __launch_bounds__(64) tile_decode_kernel(DecodeParams p) {
     store3(Gr + 4, tag, sat_add(gx.n, ga), sat_add(gx.k, gb), sat_add(gx.v, gc), lane);
   } else if (g > 0) {
     const uint64_t* Gp = p.glb + (uint64_t)(g - 1) * 8 + 4;
-    for (uint32_t spins = 0;; ++spins) {
+    for (SpinBound bound;;) {
       if (read3(Gp, tag, gx.n, gx.k, gx.v)) break;
-      if (spins > kMaxSpins) {
+      if (bound.expired()) {
         flag_timeout(p.result, lane);
         break;
       }
@@ -579,7 +596,7 @@ hipError_t launch_decode_wsc(const DecodeParams& p, void* scan_tmp, size_t scan_
                              hipStream_t s, hipStream_t aux, hipEvent_t* ev, uint64_t* carry,
                              int chunks) {
   const uint32_t nblk = p.nblk;
-  if (chunks < 1 || !aux) chunks = 1;
+  if (chunks < 1) chunks = 1;
   if (chunks > kWscMaxChunks) chunks = kWscMaxChunks;
   if ((uint32_t)chunks > nblk) chunks = (int)nblk;
   hipError_t e = hipSuccess;
@@ -602,7 +619,7 @@ hipError_t launch_decode_wsc(const DecodeParams& p, void* scan_tmp, size_t scan_
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     hipStream_t cs = s;
-    if (chunks > 1) {
+    if (chunks > 1 && aux) {
       if ((e = hipEventRecord(ev[c], s)) != hipSuccess) return e;
       if ((e = hipStreamWaitEvent(aux, ev[c], 0)) != hipSuccess) return e;
       cs = aux;
@@ -611,7 +628,7 @@ hipError_t launch_decode_wsc(const DecodeParams& p, void* scan_tmp, size_t scan_
     hipLaunchKernelGGL(wsc_copy_kernel, dim3((nb + per_wg - 1) / per_wg), dim3(256), 0, cs, q);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  if (chunks > 1) {
+  if (chunks > 1 && aux) {
     if ((e = hipEventRecord(ev[chunks], aux)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(s, ev[chunks], 0)) != hipSuccess) return e;
   }

@@ -80,7 +80,8 @@ hipError_t launch_encode(const EncodeParams& p, int num_cus, hipStream_t s);
 size_t wsc_scan_bytes(uint32_t nblk);
 // Chunked over `chunks` block ranges: walk + scan (+ carry) of chunk c on `s`, its copy on
 // `aux` after an event, so chunk c's copy overlaps chunk c+1's walk; `s` finally waits for
-// `aux`.  `ev` holds chunks + 1 events, `carry` (chunks + 1) x 3 u64 with carry[0..2] = 0.
+// `aux`.  aux == nullptr: every chunk's copy on `s` right after its walk (the copy re-reads
+// lines the walk just pulled through the 256 MiB Infinity Cache).  `ev` holds chunks + 1 events, `carry` (chunks + 1) x 3 u64 with carry[0..2] = 0.
 constexpr int kWscMaxChunks = 16;
 constexpr int kWscChunks = 1;  // default chunk count (measured: DESIGN.md)
 hipError_t launch_decode_wsc(const DecodeParams& p, void* scan_tmp, size_t scan_bytes,

@@ -1,9 +1,15 @@
-"""HBM bytes per decode launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
+"""HBM-side bytes per decode launch from rocprofv3 --pmc passes, summed over every kernel of
+the decode pipeline (walk-scan-copy: wsc_walk_kernel + rocPRIM scan of the Tri64 triples +
+wsc_copy_kernel; the single-kernel paths: lsmgpu::decode*/tile_decode).
 
-MI355X_MICROARCH.md (HBM): both counters are in KiB; on gfx950 FETCH_SIZE reports exactly half
-of the bytes of a wide coalesced streaming read -> x2.  WRITE_SIZE is exact for 16-B stores.
-Writes profiles/pmc_traffic.json, which bench.py reports as roofline.traffic when the workload
-matches.
+Reads are counted by request size -- TCC_EA0_RDREQ_{32B,64B,128B} x {32, 64, 128} B -- so no
+access-width calibration is assumed (MI355X_MICROARCH.md: FETCH_SIZE tallies 128-B requests at
+64 B; only wide streaming reads are calibrated).  Writes: TCC_EA0_WRREQ_64B x 64 B + the other
+write requests x 32 B.  FETCH_SIZE x 2 and WRITE_SIZE are kept beside them as a cross-check.
+Infinity-Cache hits are counted, not excluded (guide): at 1 GiB of input the walk's and the
+copy's reads of the same lines cannot both stay in the 256 MiB cache.
+
+usage: traffic_summary.py <rd.csv> <wr.csv> <fetch.csv> <write.csv> <bench.json> <out.json>
 """
 import csv
 import hashlib
@@ -11,18 +17,38 @@ import json
 import os
 import sys
 
-
-def kernel_values(path, counter):
-    rows = list(csv.DictReader(open(path)))
-    return [float(r["Counter_Value"]) for r in rows
-            if "lsmgpu::decode" in r["Kernel_Name"] and r["Counter_Name"] == counter]
+PIPELINE = ("lsmgpu::decode", "wsc_walk_kernel", "wsc_copy_kernel", "wsc_carry_kernel", "Tri64",
+            "tile_decode_kernel")
 
 
-def kernel_name(path):
+def per_launch(path, counters):
+    """{counter: value per decode launch}: per kernel name the median of its last 3 dispatches
+    (the timed launches come last), summed over the pipeline's kernels."""
+    vals = {}  # counter -> kernel name -> dispatch id -> value
     for r in csv.DictReader(open(path)):
-        if "lsmgpu::decode" in r["Kernel_Name"]:
-            return r["Kernel_Name"].split("(")[0]
-    return "?"
+        name, c = r["Kernel_Name"], r["Counter_Name"]
+        if c in counters and any(k in name for k in PIPELINE):
+            d = vals.setdefault(c, {}).setdefault(name, {})
+            d[int(r["Dispatch_Id"])] = d.get(int(r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
+    out = {}
+    for c in counters:
+        tot = 0.0
+        for name, disp in vals.get(c, {}).items():
+            v = [disp[k] for k in sorted(disp)][-3:]
+            tot += sorted(v)[len(v) // 2]
+        out[c] = tot
+    return out
+
+
+def kernels(path):
+    names = []
+    for r in csv.DictReader(open(path)):
+        n = r["Kernel_Name"]
+        if any(k in n for k in PIPELINE):
+            short = n.split("(")[0][:90]
+            if short not in names:
+                names.append(short)
+    return names
 
 
 def lib_sha256():
@@ -33,27 +59,34 @@ def lib_sha256():
 
 
 def main():
-    fetch_csv, write_csv, bench_json, out = sys.argv[1:5]
-    f = kernel_values(fetch_csv, "FETCH_SIZE")
-    w = kernel_values(write_csv, "WRITE_SIZE")
+    rd_csv, wr_csv, fetch_csv, write_csv, bench_json, out = sys.argv[1:7]
+    rd = per_launch(rd_csv, ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum",
+                             "TCC_EA0_RDREQ_128B_sum"))
+    wr = per_launch(wr_csv, ("TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"))
+    fs = per_launch(fetch_csv, ("FETCH_SIZE",))["FETCH_SIZE"]
+    ws = per_launch(write_csv, ("WRITE_SIZE",))["WRITE_SIZE"]
     b = json.loads(open(bench_json).read().strip().splitlines()[-1])
-    # the timed launches are the last ones (warmup first); take the median of the last 3
-    fk = sorted(f[-3:])[len(f[-3:]) // 2]
-    wk = sorted(w[-3:])[len(w[-3:]) // 2]
-    fetch_b = fk * 1024 * 2
-    write_b = wk * 1024
+    r32, r64, r128 = rd["TCC_EA0_RDREQ_32B_sum"], rd["TCC_EA0_RDREQ_64B_sum"], rd["TCC_EA0_RDREQ_128B_sum"]
+    read_b = 32 * r32 + 64 * r64 + 128 * r128
+    w64 = wr["TCC_EA0_WRREQ_64B_sum"]
+    write_b = 64 * w64 + 32 * max(0.0, wr["TCC_EA0_WRREQ_sum"] - w64)
+    alg = b["roofline"]["algorithmic_bytes_per_launch"]
     doc = {
-        "kernel": kernel_name(fetch_csv),
+        "kernels": kernels(rd_csv),
         "mode": 1,
         "workload_bytes": int(b["config"]["workload"].split(":")[1].split("B")[0].strip()),
-        "fetch_size_kib_raw": fk,
-        "write_size_kib_raw": wk,
-        "fetch_bytes_corrected": fetch_b,
-        "write_bytes": write_b,
-        "hbm_bytes_per_launch": int(fetch_b + write_b),
-        "algorithmic_bytes_per_launch": b["roofline"]["algorithmic_bytes_per_launch"],
-        "ratio_to_algorithmic": round((fetch_b + write_b) / b["roofline"]["algorithmic_bytes_per_launch"], 4),
-        "correction": "FETCH_SIZE x2 (gfx950 wide-stream undercount), KiB -> bytes",
+        "rdreq": rd,
+        "wrreq": wr,
+        "read_bytes": int(read_b),
+        "write_bytes": int(write_b),
+        "hbm_bytes_per_launch": int(read_b + write_b),
+        "algorithmic_bytes_per_launch": alg,
+        "ratio_to_algorithmic": round((read_b + write_b) / alg, 4),
+        "cross_check": {"fetch_size_kib": fs, "fetch_x2_bytes": int(fs * 2048),
+                        "write_size_kib": ws, "write_bytes": int(ws * 1024)},
+        "method": "reads 32/64/128 B x TCC_EA0_RDREQ_{32B,64B,128B}_sum; writes 64 B x WRREQ_64B + "
+                  "32 B x other WRREQ; per kernel median of the last 3 dispatches, summed over the "
+                  "decode pipeline",
         "lib_sha256": lib_sha256(),
     }
     json.dump(doc, open(out, "w"), indent=1)

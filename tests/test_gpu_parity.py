@@ -346,3 +346,47 @@ def test_wsc_split(codec, oracle, monkeypatch, split):
     data, off, ln = _sst_blocks(oracle, parts)
     _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln), f"split={split}")
     test_prefix_compressed_random(codec, oracle)
+
+
+@pytest.mark.parametrize("path", [None, "wsc", "lds"])
+def test_prefix_compressed_large_output(codec, oracle, monkeypatch, path):
+    """Prefix-compressed blocks whose OUTPUT keys exceed 64 KiB per block (plen ~ 3000 on
+    ~4000-byte... up to 60 KiB blocks of tiny entries): per-entry key offsets must not be held
+    in 16 bits.  Mixed with ordinary C2 blocks so the batch takes each path."""
+    import struct
+    if path:
+        monkeypatch.setenv("LSMGPU_DECODE_PATH", path)
+    rng = np.random.default_rng(31)
+    data = bytearray()
+    offs, lens = [], []
+    for b in range(6):
+        blk = bytearray()
+        base = bytes(rng.integers(0, 256, 3000, dtype=np.uint8))
+        n = 1 + int(rng.integers(1000, 4000))
+        prev = 0xFFFFFFFF
+        for e in range(n):
+            pos = len(blk)
+            if e == 0:
+                plen, diff, val = 0, base, b"v"
+            else:
+                plen = int(rng.integers(2000, 3001))
+                diff = bytes(rng.integers(0, 256, int(rng.integers(0, 3)), dtype=np.uint8))
+                val = bytes(rng.integers(0, 256, int(rng.integers(0, 4)), dtype=np.uint8))
+            blk += struct.pack(">HHHI", plen, len(diff), len(val), prev) + diff + val
+            prev = pos
+        blk += struct.pack(">HHHI", 0, 0, 3, prev) + b"\0\0\0"
+        assert len(blk) < 65536
+        offs.append(len(data))
+        lens.append(len(blk))
+        data += blk
+    c = _cols(2, 40000, seed=5)
+    sst, _, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, 0, 4096)
+    o2, l2, _, _ = oracle.parse_index(sst + b"{}" + (2).to_bytes(4, "big"))
+    base_off = len(data)
+    data += sst
+    off = np.concatenate([np.array(offs, np.uint32), o2 + base_off]).astype(np.uint32)
+    ln = np.concatenate([np.array(lens, np.uint32), l2]).astype(np.uint32)
+    data = bytes(data)
+    ref = oracle.decode(data, off, ln)
+    assert int(ref.key_end[int(ref.blk_first[1]) - 1]) > 65536  # the first block's keys alone
+    _assert_same(codec.decode_host(data, off, ln), ref, f"path={path}")
