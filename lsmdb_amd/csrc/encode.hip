@@ -1,14 +1,19 @@
 // encode.hip -- gfx950 SST block encode: the device restatement of Builder.Add/addHelper/
 // finishBlock/blockIndex (table/builder.go:84-160) for a sorted batch of entries.
 //
-// Every output position is closed-form, so the encoder needs no scan:
+// Every output position is closed-form, so the encoder needs no scan and no staging:
 //   entry e of block b starts at  10*e + key_start(e) + vs_start(e) + 13*b
 // (each earlier entry contributes its 10-B header, its full key -- keyDiff always returns the
 // whole key, builder.go:74-82 -- and its ValueStruct bytes; each earlier block its 13-B
-// terminator, builder.go:121-123).  One wave builds one block: it stages the block's key and
-// value bytes in LDS with coalesced loads, then writes the block as aligned 16-B chunks
-// (headers synthesised in registers), plus its restart (block end offset) in the index.
+// terminator, builder.go:121-123).  One wave per block; groups of J lanes take one entry each:
+// lane 0 of the group writes the synthesised header (8-B + 2-B stores), and the J lanes copy
+// the key and the vs-enc bytes global -> global as unaligned 16-B pieces (the last piece
+// overlapping back inside its stream, two overlapping 8/4-B pieces or single bytes below
+// 16 B), so no store crosses into a neighbour's bytes.  J follows the average entry size.
+#include <cstdlib>
+
 #include "codec_common.hpp"
+#include "decode_common.hpp"
 #include "kernels.hpp"
 
 namespace lsmgpu {
@@ -32,201 +37,165 @@ __device__ __forceinline__ void block_range(const EncodeParams& p, uint32_t b, u
   }
 }
 
-// Header byte r (0..9) of header{plen=0, klen, vlen, prev} (builder.go:30-35).
-__device__ __forceinline__ uint32_t hdr_byte(uint32_t r, uint32_t klen, uint32_t vlen,
+// big-endian stores at any alignment
+__device__ __forceinline__ void store_be32(uint8_t* d, uint32_t v) {
+  const uint32_t be = __builtin_bswap32(v);
+  __builtin_memcpy(d, &be, 4);
+}
+// header{plen = 0, klen, vlen, prev} (builder.go:23-45): 10 bytes as one 8-B + one 2-B store
+__device__ __forceinline__ void store_header(uint8_t* d, uint32_t klen, uint32_t vlen,
                                              uint32_t prev) {
-  switch (r) {
-    case 0: case 1: return 0;  // plen == 0 always (keyDiff, builder.go:74-82)
-    case 2: return (klen >> 8) & 0xff;
-    case 3: return klen & 0xff;
-    case 4: return (vlen >> 8) & 0xff;
-    case 5: return vlen & 0xff;
-    default: return (prev >> (8 * (9 - r))) & 0xff;
+  uint2 w;
+  w.x = (bswap16(klen) << 16);                    // plen 00 00 | klen BE
+  w.y = bswap16(vlen) | (bswap16(prev >> 16) << 16);  // vlen BE | prev[31:16] BE
+  __builtin_memcpy(d, &w, 8);
+  const uint16_t lo = (uint16_t)bswap16(prev & 0xffffu);
+  __builtin_memcpy(d + 8, &lo, 2);
+}
+
+// Pieces of a stream of `len` bytes and piece q of it (see the header comment).
+__device__ __forceinline__ uint32_t enc_pieces(uint32_t len) {
+  return len >= 16 ? (len + 15) >> 4 : (len >= 4 ? 2u : len);
+}
+__device__ __forceinline__ void enc_piece(uint8_t* dst, const uint8_t* src, uint32_t len,
+                                          uint32_t q) {
+  if (len >= 16) {
+    const uint32_t o = min(16 * q, len - 16);
+    uint4 v;
+    __builtin_memcpy(&v, src + o, 16);
+    __builtin_memcpy(dst + o, &v, 16);
+  } else if (len >= 8) {
+    const uint32_t o = q ? len - 8 : 0;
+    uint2 v;
+    __builtin_memcpy(&v, src + o, 8);
+    __builtin_memcpy(dst + o, &v, 8);
+  } else if (len >= 4) {
+    const uint32_t o = q ? len - 4 : 0;
+    uint32_t v;
+    __builtin_memcpy(&v, src + o, 4);
+    __builtin_memcpy(dst + o, &v, 4);
+  } else {
+    dst[q] = src[q];
   }
 }
 
-template <int SLOT, int MAXE, int WPB>
-struct EncodeCfg {
-  static constexpr int kData = SLOT + 64;
-  static constexpr int kMeta = (MAXE + 2) * 8;
-  static constexpr int kWaveBytes = (kData + kMeta + 15) & ~15;
-  static constexpr int kLds = kWaveBytes * WPB;
-};
-
-// Slow path: byte-granular writes straight from global memory (blocks too large for LDS).
-__device__ void encode_block_slow(const EncodeParams& p, uint32_t b, uint64_t f, uint64_t l,
-                                  uint64_t bs, uint32_t lane) {
-  uint64_t pos = bs;
-  uint32_t prev = 0xffffffffu;
-  const uint64_t k0 = key_start(p, f), v0 = vs_start(p, f);
-  for (uint64_t e = f; e <= l; e++) {
-    uint32_t klen, vlen;
-    uint64_t ks = 0, vss = 0;
-    if (e < l) {
-      ks = key_start(p, e);
-      vss = vs_start(p, e);
-      klen = (uint32_t)(p.key_end[e] - ks);
-      vlen = (uint32_t)(p.vs_end[e] - vss);
-    } else {
-      klen = 0;
-      vlen = 3;
-    }
-    uint32_t total = 10 + klen + vlen;
-    for (uint32_t i = lane; i < total; i += kWave) {
-      uint32_t byte;
-      if (i < 10) byte = hdr_byte(i, klen, vlen, prev);
-      else if (i < 10 + klen) byte = p.keys[ks + (i - 10)];
-      else byte = (e < l) ? p.vs[vss + (i - 10 - klen)] : 0;
-      p.out[pos + i] = (uint8_t)byte;
-    }
-    prev = (uint32_t)(pos - bs);
-    pos += total;
-  }
-  (void)k0; (void)v0; (void)b;
-}
-
-template <int SLOT, int MAXE, int WPB>
-__global__ void __launch_bounds__(WPB * 64) encode_kernel(EncodeParams p) {
-  using Cfg = EncodeCfg<SLOT, MAXE, WPB>;
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+template <uint32_t J, uint32_t G>
+__global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
+  constexpr uint32_t EPP = kWave / J;      // entries per group pass; G group passes per loop
+                                           // trip, every offset load issued first
   const uint32_t lane = lane_id();
-  const uint32_t wv = threadIdx.x >> 6;
-  uint8_t* slot = smem + wv * Cfg::kWaveBytes;
-  uint16_t* meta = reinterpret_cast<uint16_t*>(slot + Cfg::kData);
-  const uint32_t nwaves = gridDim.x * WPB;
+  const uint32_t b = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (b >= p.nblocks) return;
+  uint64_t f, l;
+  block_range(p, b, f, l);
+  f = uniform64(f);
+  l = uniform64(l);
+  const uint64_t m = l - f;
+  const uint32_t blk13 = 13u * b;
 
-  for (uint32_t b = blockIdx.x * WPB + wv; b < p.nblocks; b += nwaves) {
-    uint64_t f, l;
-    block_range(p, b, f, l);
-    f = uniform64(f);
-    l = uniform64(l);
-    const uint64_t kf = uniform64(key_start(p, f)), kl = uniform64(key_start(p, l));
-    const uint64_t vf = uniform64(vs_start(p, f)), vl = uniform64(vs_start(p, l));
-    const uint64_t m = l - f;
-    const uint64_t bs = 10 * f + kf + vf + 13ull * b;       // block start
-    const uint64_t bsize = 10 * m + (kl - kf) + (vl - vf) + 13;
-    const uint64_t be = bs + bsize;                          // block end = restart value
-
-    // entry validation (y.go:93-100 ParseKey needs len(key) > 8; vlen is a uint16)
-    uint32_t bad = 0;
-    for (uint64_t e = f + lane; e < l; e += kWave) {
-      uint64_t klen = p.key_end[e] - key_start(p, e), vlen = p.vs_end[e] - vs_start(p, e);
-      if (klen <= 8 || klen > 0xffff) bad |= 1;
-      if (vlen > 0xffff) bad |= 2;
+  if (m == 0) {  // a block of no entries: the terminator alone (table_test.go:514)
+    if (lane == 0) {
+      const uint32_t bs = (uint32_t)(10 * f + key_start(p, f) + vs_start(p, f)) + blk13;
+      uint8_t* t = p.out + bs;
+      store_header(t, 0, 3, 0xffffffffu);
+      t[10] = 0;
+      t[11] = 0;
+      t[12] = 0;
+      store_be32(p.out + p.data_len + 4ull * b, bs + 13);
     }
-    if (bad) atomicOr(p.flags, bad);
-
-    // restart entry of the index (builder.go:146-160), BE32, byte stores (any alignment)
-    if (lane < 4) p.out[p.data_len + 4ull * b + lane] = (uint8_t)((uint32_t)be >> (8 * (3 - lane)));
-    if (b == p.nblocks - 1 && lane >= 4 && lane < 8)
-      p.out[p.data_len + 4ull * p.nblocks + (lane - 4)] =
-          (uint8_t)(p.nblocks >> (8 * (7 - lane)));
-
-    const uint64_t nk = kl - kf, nv = vl - vf;
-    const bool fast = (m <= (uint64_t)MAXE) && (bsize <= 0xffffull) && (nk + nv + 48 <= (uint64_t)Cfg::kData);
-    if (!fast) {
-      encode_block_slow(p, b, f, l, bs, lane);
-      continue;
-    }
-    // stage keys at slot[shk..], values at slot[vbase + shv..]
-    const uint32_t shk = stage_to_lds(slot, p.keys, kf, (uint32_t)nk, p.key_total, lane);
-    const uint32_t vbase = (uint32_t)((shk + nk + 15) & ~15ull);
-    const uint32_t shv = stage_to_lds(slot + vbase, p.vs, vf, (uint32_t)nv, p.vs_total, lane);
-    const uint32_t vsrc = vbase + shv;
-    // meta row i (i <= m): {pos in block, key off in LDS, vs off in LDS, 0}; row m = terminator
-    for (uint32_t i = lane; i <= (uint32_t)m; i += kWave) {
-      uint64_t e = f + i;
-      uint32_t ko = (uint32_t)(key_start(p, e) - kf), vo = (uint32_t)(vs_start(p, e) - vf);
-      uint32_t pos = 10 * i + ko + vo;
-      *reinterpret_cast<ushort4*>(meta + 4 * i) =
-          make_ushort4((uint16_t)pos, (uint16_t)(shk + ko), (uint16_t)(vsrc + vo), 0);
-    }
-    if (lane == 0)  // row m+1: end sentinel (terminator value bytes are zeros, see below)
-      *reinterpret_cast<ushort4*>(meta + 4 * (m + 1)) =
-          make_ushort4((uint16_t)bsize, (uint16_t)(shk + nk), (uint16_t)(vsrc + nv), 0);
-    wave_lds_fence();
-
-    // gather-write the block [bs, be) in aligned 16-B chunks
-    uint8_t* dst = p.out + bs;
-    const uint32_t h = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);
-    uint8_t* dal = dst - h;
-    const uint32_t L = (uint32_t)bsize;
-    const uint32_t nchunk = (h + L + 15) >> 4;
-    for (uint32_t c = lane; c < nchunk; c += kWave) {
-      const int32_t t0 = (int32_t)(c * 16) - (int32_t)h;
-      const int32_t lo = t0 < 0 ? 0 : t0;
-      const int32_t hi = (t0 + 16 > (int32_t)L) ? (int32_t)L : t0 + 16;
-      uint32_t e = meta_search(meta, (uint32_t)m + 1, (uint32_t)lo);
-      ushort4 me = *reinterpret_cast<const ushort4*>(meta + 4 * e);
-      ushort4 mn = *reinterpret_cast<const ushort4*>(meta + 4 * e + 4);
-      const bool full = (lo == t0) && (hi == t0 + 16);
-      if (full && e < m) {
-        uint32_t klen = (uint32_t)mn.y - me.y;
-        uint32_t r0 = (uint32_t)t0 - me.x;
-        uint32_t tend = (uint32_t)mn.x;  // next entry start
-        if (r0 >= 10 && r0 + 16 <= 10 + klen) {
-          *reinterpret_cast<uint4*>(dal + 16 * c) = lds_u128(slot, me.y + r0 - 10);
-          continue;
-        }
-        if (r0 >= 10 + klen && (uint32_t)t0 + 16 <= tend) {
-          *reinterpret_cast<uint4*>(dal + 16 * c) = lds_u128(slot, me.z + (r0 - 10 - klen));
-          continue;
-        }
-      }
-      uint4 v = make_uint4(0, 0, 0, 0);
-      uint32_t prev = 0xffffffffu;
-      if (e > 0) prev = meta[4 * (e - 1)];
-#pragma unroll
-      for (int i = 0; i < 16; i++) {
-        const int32_t t = t0 + i;
-        if (t < lo || t >= hi) continue;
-        while (e < m && (uint32_t)mn.x <= (uint32_t)t) {
-          prev = me.x;
-          e++;
-          me = mn;
-          mn = *reinterpret_cast<const ushort4*>(meta + 4 * e + 4);
-        }
-        uint32_t r = (uint32_t)t - me.x;
-        uint32_t klen = (e < m) ? (uint32_t)mn.y - me.y : 0;
-        uint32_t vlen = (e < m) ? (uint32_t)mn.z - me.z : 3;
-        uint32_t byte;
-        if (r < 10) byte = hdr_byte(r, klen, vlen, prev);
-        else if (r < 10 + klen) byte = slot[me.y + r - 10];
-        else byte = (e < m) ? slot[me.z + (r - 10 - klen)] : 0;
-        if (full) set_byte(v, i, byte);
-        else dal[16 * c + i] = (uint8_t)byte;
-      }
-      if (full) *reinterpret_cast<uint4*>(dal + 16 * c) = v;
-    }
-    wave_lds_fence();
+    if (lane == 1 && b == p.nblocks - 1) store_be32(p.out + p.data_len + 4ull * p.nblocks, p.nblocks);
+    return;
   }
+  if (lane == 1 && b == p.nblocks - 1) store_be32(p.out + p.data_len + 4ull * p.nblocks, p.nblocks);
+
+  // Absolute entry positions are closed-form (no block base needed to place bytes); the block
+  // start is entry f's position (lane 0, first pass), a header's prev is the previous entry's
+  // position (the neighbouring lane group, or the previous pass), and the lane group holding
+  // the block's last entry writes the terminator and the restart.
+  const uint32_t j = lane & (J - 1);
+  uint32_t bad = 0, bs = 0, carry = 0;
+  for (uint64_t e0 = 0; e0 < m; e0 += (uint64_t)G * EPP) {
+    uint32_t klen[G], vlen[G], pos[G], np[G], kp[G];
+    uint64_t ks[G], vs0[G];
+    bool on[G];
+#pragma unroll
+    for (uint32_t i = 0; i < G; i++) {
+      const uint64_t r = e0 + i * EPP + lane / J;  // entry index inside the block
+      on[i] = r < m;
+      const uint64_t e = f + (on[i] ? r : m - 1);
+      ks[i] = key_start(p, e);
+      vs0[i] = vs_start(p, e);
+      const uint64_t kl64 = p.key_end[e] - ks[i], vl64 = p.vs_end[e] - vs0[i];
+      klen[i] = (uint32_t)kl64;
+      vlen[i] = (uint32_t)vl64;
+      pos[i] = (uint32_t)(10 * e + ks[i] + vs0[i]) + blk13;
+      if (on[i] && j == 0) {
+        if (kl64 <= 8 || kl64 > 0xffff) bad |= 1;  // ParseKey needs len(key) > 8 (y.go:93-100)
+        if (vl64 > 0xffff) bad |= 2;                // header vlen is a uint16
+      }
+      kp[i] = enc_pieces(klen[i]);
+      np[i] = on[i] ? kp[i] + enc_pieces(vlen[i]) : 0u;
+    }
+    if (e0 == 0) bs = readlane(pos[0], 0);
+#pragma unroll
+    for (uint32_t i = 0; i < G; i++) {
+      // previous entry's position: the lane group below, else the previous group / pass
+      const uint32_t below = __shfl_up(pos[i], J);
+      const uint32_t edge = i == 0 ? carry : readlane(pos[i - 1], kWave - J);
+      const uint64_t r = e0 + i * EPP + lane / J;
+      const uint32_t prev = r == 0 ? 0xffffffffu : (lane < J ? edge : below) - bs;  // builder.go:95-99
+      if (on[i] && j == 0) store_header(p.out + pos[i], klen[i], vlen[i], prev);
+      if (on[i] && j == 1 && r == m - 1) {  // terminator + restart (builder.go:121-123,146-160)
+        const uint32_t te = pos[i] + 10 + klen[i] + vlen[i];
+        uint8_t* t = p.out + te;
+        store_header(t, 0, 3, pos[i] - bs);
+        t[10] = 0;
+        t[11] = 0;
+        t[12] = 0;
+        store_be32(p.out + p.data_len + 4ull * b, te + 13);
+      }
+    }
+    carry = readlane(pos[G - 1], kWave - J);
+#pragma unroll
+    for (uint32_t i = 0; i < G; i++) {
+      for (uint32_t q = j; q < np[i]; q += J) {  // one (non-divergent) copy per piece
+        const bool key = q < kp[i];
+        enc_piece(p.out + pos[i] + 10 + (key ? 0u : klen[i]), key ? p.keys + ks[i] : p.vs + vs0[i],
+                  key ? klen[i] : vlen[i], key ? q : q - kp[i]);
+      }
+    }
+  }
+  if (bad) atomicOr(p.flags, bad);
 }
 
-template <int SLOT, int MAXE, int WPB>
-static hipError_t launch_enc(const EncodeParams& p, int num_cus, hipStream_t s) {
-  using Cfg = EncodeCfg<SLOT, MAXE, WPB>;
-  auto k = encode_kernel<SLOT, MAXE, WPB>;
-  int per_cu = 0;
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, WPB * 64, Cfg::kLds);
-  if (e != hipSuccess) return e;
-  if (per_cu < 1) per_cu = 1;
-  uint64_t want = ((uint64_t)p.nblocks + WPB - 1) / WPB;
-  uint64_t grid = (uint64_t)per_cu * (uint64_t)num_cus;
-  if (grid > want) grid = want;
-  if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(WPB * 64), Cfg::kLds, s, p);
+template <uint32_t J, uint32_t G>
+static hipError_t launch_enc(const EncodeParams& p, hipStream_t s) {
+  hipLaunchKernelGGL((encode_kernel<J, G>), dim3((p.nblocks + 3) / 4), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
 hipError_t launch_encode(const EncodeParams& p, int num_cus, hipStream_t s) {
-  // the slot holds one block's key + value bytes
-  if (p.vs_total + p.key_total == 0 || true) {
-    // choose by the average block payload when no exact bound is known
-    uint64_t payload = (p.key_total + p.vs_total) / (p.nblocks ? p.nblocks : 1);
-    if (payload + 64 <= 3072) return launch_enc<4096, 128, 4>(p, num_cus, s);
-    if (payload + 64 <= 12288) return launch_enc<16384, 512, 2>(p, num_cus, s);
+  (void)num_cus;
+  // J = lanes per entry ~ the average entry's 16-B pieces (C2: 129 B -> 8; C3: ~1.1 KB -> 64)
+  const uint64_t avg = p.n ? (p.key_total + p.vs_total) / p.n : 0;
+  const char* ge = getenv("LSMGPU_ENC_G");  // A/B: entry-group passes per loop trip
+  const int g = ge ? atoi(ge) : 1;           // measured: C2 G=1 0.61 ms, 2 0.68, 4 0.72
+  const char* je = getenv("LSMGPU_ENC_J");   // A/B: lanes per entry
+  if (je) {
+    const int jj = atoi(je);
+    if (jj == 4) return launch_enc<4, 1>(p, s);
+    if (jj == 16) return launch_enc<16, 1>(p, s);
+    if (jj == 8) return launch_enc<8, 1>(p, s);
   }
-  return launch_enc<32768, 1024, 1>(p, num_cus, s);
+  // measured (1 GiB): C2 (119 B entries) J=8 0.57 ms vs J=4 0.63 / J=16 0.73; C5 (~141 B)
+  // J=16 0.88 ms vs J=8 0.96
+  if (g == 4) return avg <= 128 ? launch_enc<8, 4>(p, s) : launch_enc<16, 4>(p, s);
+  if (g == 2) return avg <= 128 ? launch_enc<8, 2>(p, s) : launch_enc<16, 2>(p, s);
+  if (avg <= 48) return launch_enc<4, 1>(p, s);
+  if (avg <= 128) return launch_enc<8, 1>(p, s);
+  if (avg <= 496) return launch_enc<16, 1>(p, s);
+  if (avg <= 1008) return launch_enc<32, 1>(p, s);
+  return launch_enc<64, 1>(p, s);
 }
 
 // ---------------------------------------------------------------- ValueStruct columns
