@@ -290,6 +290,9 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     uint32_t split = max_blk_len > 8192 ? 2u : 1u;  // measured: C5 1.25 -> 1.09 ms at 2
     if (sp_env) split = (uint32_t)atoi(sp_env);
     p.wsplit = (split == 2 || split == 4) ? split : 1u;
+    const char* j_env = getenv("LSMGPU_WSC_J");  // A/B: lanes per entry in the copy
+    p.wj = j_env ? (uint32_t)atoi(j_env) : 0u;
+    if (p.wj != 8 && p.wj != 16) p.wj = 0;
     const bool one_stream = getenv("LSMGPU_WSC_ONE_STREAM") != nullptr;
     HIPC(launch_decode_wsc(p, c->wsc_tmp.p, c->wsc_tmp.cap, c->stream,
                            one_stream ? nullptr : c->aux, c->wev,

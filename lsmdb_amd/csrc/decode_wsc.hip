@@ -17,6 +17,8 @@
 //                    no store leaves it) global -> global, plus end offsets / view records
 // Traffic: the input is read twice (walk touches every line; copy reads the bytes) -- the
 // price of taking the serial walk off the critical path.  Blocks must be < 64 KiB.
+#include <cstdlib>
+
 #include <rocprim/device/device_scan.hpp>
 
 #include "codec_common.hpp"
@@ -161,7 +163,79 @@ __device__ __forceinline__ void piece_copy(uint8_t* dst, const uint8_t* src, uin
   }
 }
 
-// K2: one wave per block, J = 8 lanes per entry.
+// The entries of one block: J lanes per entry; an entry's pieces are [key pieces | value
+// pieces] (16 B, the last overlapping back inside its stream, or two overlapping 8/4/2/1-B
+// pieces below 16 B) and lane j takes pieces j, j + J, ...  G entry groups per pass, all
+// metadata loads issued first.
+template <uint32_t J, uint32_t G>
+__device__ __forceinline__ void copy_entries(const DecodeParams& p, const uint2* meta,
+                                             const uint8_t* blk, uint8_t* kbase, uint8_t* vbase,
+                                             uint32_t n, uint64_t en, uint64_t ek, uint64_t ev,
+                                             uint32_t off, uint32_t sub, uint32_t split,
+                                             bool mat, bool view, uint32_t lane) {
+  const uint32_t j = lane & (J - 1);
+  bool any_plen = false;
+  for (uint32_t e0 = sub * G * (kWave / J); e0 < n; e0 += split * G * (kWave / J)) {
+    uint32_t hp[G], kl[G], vl[G], ko[G], vo[G], np[G], kp[G];
+    bool on[G];
+#pragma unroll
+    for (int i = 0; i < G; i++) {
+      const uint32_t e = e0 + i * (kWave / J) + (lane / J);
+      const uint32_t ec = min(e, n - 1);
+      const uint2 m0 = meta[ec], m1 = meta[ec + 1];
+      hp[i] = m0.x & 0xffffu;
+      vo[i] = m0.x >> 16;
+      ko[i] = m0.y;
+      const uint32_t ko1 = m1.y, vo1 = m1.x >> 16;
+      vl[i] = vo1 - vo[i];
+      kl[i] = (m1.x & 0xffffu) - hp[i] - 10 - vl[i];  // stored key bytes
+      const uint32_t plen = ko1 - ko[i] - kl[i];
+      on[i] = e < n;
+      any_plen = any_plen || (on[i] && plen != 0);
+      kp[i] = plen ? 0u : n_pieces16(kl[i]);  // prefix-compressed keys: bytewise pass below
+      np[i] = kp[i] + n_pieces16(vl[i]);
+      if (on[i] && j == 0) {
+        if (mat) {
+          if (p.key_end) p.key_end[en + e] = (uint32_t)(ek + ko1);
+          if (p.val_end) p.val_end[en + e] = (uint32_t)(ev + vo1);
+        }
+        if (view)
+          p.view[en + e] = (uint64_t)(off + hp[i] + 10) | ((uint64_t)kl[i] << 32) |
+                           ((uint64_t)vl[i] << 48);
+      }
+    }
+    if (!mat) continue;
+#pragma unroll
+    for (int i = 0; i < G; i++) {
+      if (!on[i]) continue;
+      for (uint32_t q = j; q < np[i]; q += J) {
+        const bool key = q < kp[i];
+        const uint32_t len = key ? kl[i] : vl[i];
+        uint8_t* dst = key ? kbase : vbase;
+        if (!dst) continue;
+        const uint32_t s0 = key ? hp[i] + 10 : hp[i] + 10 + kl[i];
+        piece_copy(dst + (key ? ko[i] : vo[i]), blk + s0, len, key ? q : q - kp[i]);
+      }
+    }
+  }
+  if (any_plen && kbase && mat) {  // baseKey[:plen] ++ diff (iterator.go:98-100): bytewise
+    // the same passes as above (any_plen covers only this wave's entries)
+    for (uint32_t e = sub * G * (kWave / J) + (lane / J); e < n;
+         e += ((e / (kWave / J)) % G == G - 1) ? (split - 1) * G * (kWave / J) + kWave / J
+                                              : kWave / J) {
+      const uint2 m0 = meta[e], m1 = meta[e + 1];
+      const uint32_t hp = m0.x & 0xffffu, ko = m0.y;
+      const uint32_t vl = (m1.x >> 16) - (m0.x >> 16);
+      const uint32_t kl = m1.y - ko;                                // output key bytes
+      const uint32_t plen = kl - ((m1.x & 0xffffu) - hp - 10 - vl);
+      if (plen == 0) continue;
+      for (uint32_t i = j; i < kl; i += J)
+        kbase[ko + i] = i < plen ? blk[10 + i] : blk[hp + 10 + i - plen];
+    }
+  }
+}
+
+// K2: one wave per block (p.wsplit waves above 8 KiB).
 __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   const uint32_t lane = lane_id();
   // p.wsplit waves share a block (large blocks): wave `sub` takes passes sub, sub + wsplit, ...
@@ -208,70 +282,13 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   const uint2* meta = reinterpret_cast<const uint2*>(p.wmeta) + (uint64_t)b * p.wcap;
   uint8_t* kbase = p.key_data ? p.key_data + ek : nullptr;
   uint8_t* vbase = p.val_data ? p.val_data + ev : nullptr;
-  // J = 8 lanes per entry; an entry's pieces are [key pieces | value pieces] (16 B, the last
-  // overlapping back inside its stream, or two overlapping 8/4/2/1-B pieces below 16 B) and
-  // lane j takes pieces j, j + 8, ...  Four entry groups per pass, all loads issued first.
-  constexpr uint32_t J = 8, G = 4;
-  const uint32_t j = lane & (J - 1);
-  bool any_plen = false;
-  for (uint32_t e0 = sub * G * (kWave / J); e0 < n; e0 += split * G * (kWave / J)) {
-    uint32_t hp[G], kl[G], vl[G], ko[G], vo[G], np[G], kp[G];
-    bool on[G];
-#pragma unroll
-    for (int i = 0; i < G; i++) {
-      const uint32_t e = e0 + i * (kWave / J) + (lane >> 3);
-      const uint32_t ec = min(e, n - 1);
-      const uint2 m0 = meta[ec], m1 = meta[ec + 1];
-      hp[i] = m0.x & 0xffffu;
-      vo[i] = m0.x >> 16;
-      ko[i] = m0.y;
-      const uint32_t ko1 = m1.y, vo1 = m1.x >> 16;
-      vl[i] = vo1 - vo[i];
-      kl[i] = (m1.x & 0xffffu) - hp[i] - 10 - vl[i];  // stored key bytes
-      const uint32_t plen = ko1 - ko[i] - kl[i];
-      on[i] = e < n;
-      any_plen = any_plen || (on[i] && plen != 0);
-      kp[i] = plen ? 0u : n_pieces16(kl[i]);  // prefix-compressed keys: bytewise pass below
-      np[i] = kp[i] + n_pieces16(vl[i]);
-      if (on[i] && j == 0) {
-        if (mat) {
-          if (p.key_end) p.key_end[en + e] = (uint32_t)(ek + ko1);
-          if (p.val_end) p.val_end[en + e] = (uint32_t)(ev + vo1);
-        }
-        if (view)
-          p.view[en + e] = (uint64_t)(off + hp[i] + 10) | ((uint64_t)kl[i] << 32) |
-                           ((uint64_t)vl[i] << 48);
-      }
-    }
-    if (!mat) continue;
-#pragma unroll
-    for (int i = 0; i < G; i++) {
-      if (!on[i]) continue;
-      for (uint32_t q = j; q < np[i]; q += J) {
-        const bool key = q < kp[i];
-        const uint32_t len = key ? kl[i] : vl[i];
-        uint8_t* dst = key ? kbase : vbase;
-        if (!dst) continue;
-        const uint32_t s0 = key ? hp[i] + 10 : hp[i] + 10 + kl[i];
-        piece_copy(dst + (key ? ko[i] : vo[i]), blk + s0, len, key ? q : q - kp[i]);
-      }
-    }
-  }
-  if (any_plen && kbase && mat) {  // baseKey[:plen] ++ diff (iterator.go:98-100): bytewise
-    // the same passes as above (any_plen covers only this wave's entries)
-    for (uint32_t e = sub * G * (kWave / J) + (lane >> 3); e < n;
-         e += ((e / (kWave / J)) % G == G - 1) ? (split - 1) * G * (kWave / J) + kWave / J
-                                              : kWave / J) {
-      const uint2 m0 = meta[e], m1 = meta[e + 1];
-      const uint32_t hp = m0.x & 0xffffu, ko = m0.y;
-      const uint32_t vl = (m1.x >> 16) - (m0.x >> 16);
-      const uint32_t kl = m1.y - ko;                                // output key bytes
-      const uint32_t plen = kl - ((m1.x & 0xffffu) - hp - 10 - vl);
-      if (plen == 0) continue;
-      for (uint32_t i = j; i < kl; i += J)
-        kbase[ko + i] = i < plen ? blk[10 + i] : blk[hp + 10 + i - plen];
-    }
-  }
+  // lanes per entry from this block's average entry (known after the walk): 8 for C2-like
+  // 119-B entries, 16 above 128 B (C5 Zipf keys: 0.96 vs 1.10 ms); p.wj forces 8 or 16
+  const uint32_t avg = (K + V) / n;
+  if (p.wj == 16 || (p.wj == 0 && avg > 128))
+    copy_entries<16, 2>(p, meta, blk, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane);
+  else
+    copy_entries<8, 4>(p, meta, blk, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane);
 }
 
 

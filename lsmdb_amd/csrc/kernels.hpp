@@ -42,6 +42,7 @@ struct DecodeParams {
   uint32_t* wstatus;
   uint32_t wb0, wb1;        // walk-scan-copy: this launch's block range [wb0, wb1)
   uint32_t wsplit;          // walk-scan-copy: waves per block in the copy (1, 2 or 4)
+  uint32_t wj;              // walk-scan-copy: lanes per entry forced (8, 16), 0 = per block
 };
 
 // Encode: one wave per output block; every byte position is closed-form
