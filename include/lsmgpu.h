@@ -148,6 +148,48 @@ int lsmgpu_encode_values(lsmgpu_ctx* ctx, const uint8_t* meta, const uint8_t* us
                          const uint32_t* value_end, uint64_t n, int on_device, uint8_t* vs,
                          uint64_t vs_cap, uint32_t* vs_end, uint64_t* vs_len);
 
+/* ---- Batched OpenTable index work on the device ----------------------
+ * Replaces, for ntables SSTs resident in device memory at once, what OpenTable does per table
+ * on the host (table/table.go:88-144): readIndex (table.go:177-269: tail parse, every block's
+ * first header + first key with the plen == 0 assertion -- the 64-goroutine fan-out -- and
+ * sort.Sort(byKey) of the block index by y.CompareKeys), then smallest = a forward iterator's
+ * Rewind (first entry of the first sorted block, iterator.go:201-217) and biggest = a reversed
+ * iterator's Rewind (SeekToLast of the last sorted block: forward walk, then Prev() through the
+ * last decoded header's `prev`, iterator.go:86-91,137-155,219-235).
+ * Table t is data[sst_off[t], sst_off[t] + sst_len[t]); every offset below is relative to it.
+ * Keys are views: first key i = table[key_off[i], +key_len[i]); smallest = table[off, +len];
+ * biggest = table[base_off, +plen] ++ table[diff_off, +klen] (baseKey[:plen] ++ diff -- Go's
+ * block slices are windows of the mmap'd file, so these may extend past the block). */
+#define LSMGPU_TBL_OK 0
+#define LSMGPU_TBL_BAD_TAIL 1    /* malformed tail / restarts (lsmgpu_parse_index's BAD_TAIL)    */
+#define LSMGPU_TBL_FIRST_PLEN 2  /* a block's first header has plen != 0 (table.go:239 panic)    */
+#define LSMGPU_TBL_READ 3        /* first header/key past the file (table.go:226-237 read error) */
+#define LSMGPU_TBL_KEY_LEN 4     /* a first key of <= 8 B compared by the sort (y.go:85 panic)   */
+#define LSMGPU_TBL_CAPACITY 5    /* the batch has more blocks than blk_cap                       */
+#define LSMGPU_TBL_BIGGEST 6     /* SeekToLast/Prev would panic (read past the file); no biggest */
+typedef struct {
+  /* per table [ntables] */
+  uint32_t* nblk;         /* restart count N (table.go:188-199)                                  */
+  uint32_t* blk_base;     /* [ntables + 1]: table t's blocks are entries [blk_base[t], blk_base[t+1]) */
+  uint32_t* bloom_off;    /* bloom JSON span (table.go:181-186)                                  */
+  uint32_t* bloom_len;
+  int32_t* status;        /* LSMGPU_TBL_*; the outputs below are defined when OK or BIGGEST      */
+  uint32_t* smallest;     /* 3 per table: {has, off, len}                                        */
+  uint32_t* biggest;      /* 5 per table: {has, base_off, plen, diff_off, klen}                  */
+  /* per block [blk_cap], SST order within each table */
+  uint32_t* blk_off;      /* Table.blockIndex offsets / lengths (table.go:202-215)               */
+  uint32_t* blk_len;
+  uint32_t* key_off;      /* the block's first key (blockIndex key, table.go:236-246)            */
+  uint32_t* key_len;
+  uint32_t* order;        /* sorted blockIndex: order[blk_base[t] + i] = SST index of block i    */
+  uint64_t blk_cap;
+} lsmgpu_tables;
+/* Device pointers only; asynchronous on the context's stream.  d_result (device, 8 u64):
+ * [0] total blocks, [1] tables whose status is not LSMGPU_TBL_OK. */
+int lsmgpu_open_tables_async(lsmgpu_ctx* ctx, const uint8_t* d_data, uint64_t data_len,
+                             const uint64_t* d_sst_off, const uint64_t* d_sst_len,
+                             uint32_t ntables, const lsmgpu_tables* out, uint64_t* d_result);
+
 #ifdef __cplusplus
 }
 #endif

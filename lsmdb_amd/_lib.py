@@ -47,6 +47,7 @@ EXPORTED_SYMBOLS = (
     "lsmgpu_strerror",
     "lsmgpu_abi_version",
     "lsmgpu_parse_index",
+    "lsmgpu_open_tables_async",
     "lsmgpu_decode_blocks",
     "lsmgpu_decode_blocks_async",
     "lsmgpu_encode_blocks",
@@ -73,6 +74,25 @@ class LsmgpuDecoded(ctypes.Structure):
         ("val_bytes", c_uint64),
         ("first_bad_block", c_int64),
         ("n_bad_blocks", c_uint64),
+    ]
+
+
+class Tables(ctypes.Structure):
+    """lsmgpu_tables (include/lsmgpu.h): batched OpenTable outputs, device pointers."""
+    _fields_ = [
+        ("nblk", c_void_p),
+        ("blk_base", c_void_p),
+        ("bloom_off", c_void_p),
+        ("bloom_len", c_void_p),
+        ("status", c_void_p),
+        ("smallest", c_void_p),
+        ("biggest", c_void_p),
+        ("blk_off", c_void_p),
+        ("blk_len", c_void_p),
+        ("key_off", c_void_p),
+        ("key_len", c_void_p),
+        ("order", c_void_p),
+        ("blk_cap", c_uint64),
     ]
 
 
@@ -140,6 +160,9 @@ def _load() -> ctypes.CDLL:
                                          c_uint64, c_int, c_void_p, c_uint64, c_void_p,
                                          POINTER(c_uint64)]
     lib.lsmgpu_encode_values.restype = c_int
+    lib.lsmgpu_open_tables_async.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p,
+                                             c_uint32, POINTER(Tables), c_void_p]
+    lib.lsmgpu_open_tables_async.restype = c_int
     return lib
 
 

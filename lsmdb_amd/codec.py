@@ -273,6 +273,70 @@ class Codec:
         return out[: ln.value].tobytes(), end
 
 
+    # -- batched table open (OpenTable index work, table.go:88-144,177-269)
+    def open_tables_device(self, data, sst_off, sst_len, blk_cap: int) -> dict:
+        """ntables SSTs resident in `data` (device u8 tensor), table t = data[sst_off[t]:
+        +sst_len[t]] (device i64 tensors).  Returns the device output tensors (asynchronous on
+        the codec's stream); see lsmgpu_tables in include/lsmgpu.h."""
+        import torch
+        dev = data.device
+        nt = sst_off.numel()
+        i32 = dict(dtype=torch.int32, device=dev)
+        o = dict(nblk=torch.empty(max(nt, 1), **i32), blk_base=torch.empty(nt + 1, **i32),
+                 bloom_off=torch.empty(max(nt, 1), **i32), bloom_len=torch.empty(max(nt, 1), **i32),
+                 status=torch.empty(max(nt, 1), **i32), smallest=torch.empty(3 * max(nt, 1), **i32),
+                 biggest=torch.empty(5 * max(nt, 1), **i32),
+                 blk_off=torch.empty(max(blk_cap, 1), **i32), blk_len=torch.empty(max(blk_cap, 1), **i32),
+                 key_off=torch.empty(max(blk_cap, 1), **i32), key_len=torch.empty(max(blk_cap, 1), **i32),
+                 order=torch.empty(max(blk_cap, 1), **i32),
+                 result=torch.zeros(8, dtype=torch.int64, device=dev))
+        st = _lib.Tables(*[_ptr(o[k]) for k in ("nblk", "blk_base", "bloom_off", "bloom_len", "status",
+                                                "smallest", "biggest", "blk_off", "blk_len",
+                                                "key_off", "key_len", "order")], blk_cap)
+        check(lib().lsmgpu_open_tables_async(self._ctx, _ptr(data), data.numel(), _ptr(sst_off),
+                                             _ptr(sst_len), nt, byref(st), _ptr(o["result"])),
+              "open_tables_async")
+        return o
+
+    def open_tables_host(self, ssts, blk_cap: Optional[int] = None) -> list:
+        """OpenTable's index work for a list of SST images (bytes) in one batch on the GPU.
+        Per table: status, nblk, bloom span, blk_off/blk_len/key_off/key_len/order (numpy,
+        table-relative), smallest / biggest (bytes or None)."""
+        import torch
+        raws = [bytes(x) for x in ssts]
+        offs, pos = [], 0
+        for r in raws:
+            offs.append(pos)
+            pos += len(r)
+        buf = np.frombuffer(b"".join(raws) + b"\0" * 16, np.uint8)
+        if blk_cap is None:
+            blk_cap = sum(max(len(r) // 13, 1) for r in raws)  # a block is >= 13 B
+        d = torch.from_numpy(buf.copy()).to(self.device)
+        d_off = torch.tensor(offs, dtype=torch.int64, device=self.device)
+        d_len = torch.tensor([len(r) for r in raws], dtype=torch.int64, device=self.device)
+        o = self.open_tables_device(d, d_off, d_len, blk_cap)
+        self.synchronize()
+        h = {k: v.cpu().numpy().view(np.uint32) for k, v in o.items() if k != "result"}
+        out = []
+        for t, r in enumerate(raws):
+            b0, b1 = int(h["blk_base"][t]), int(h["blk_base"][t + 1])
+            stt = int(h["status"].view(np.int32)[t])
+            sm, bg = h["smallest"][3 * t: 3 * t + 3], h["biggest"][5 * t: 5 * t + 5]
+            ok = stt in (0, 6)
+            out.append(dict(
+                status=stt, nblk=int(h["nblk"][t]), bloom_off=int(h["bloom_off"][t]),
+                bloom_len=int(h["bloom_len"][t]),
+                blk_off=h["blk_off"][b0:b1].copy() if ok else None,
+                blk_len=h["blk_len"][b0:b1].copy() if ok else None,
+                key_off=h["key_off"][b0:b1].copy() if ok else None,
+                key_len=h["key_len"][b0:b1].copy() if ok else None,
+                order=h["order"][b0:b1].copy() if ok else None,
+                smallest=r[int(sm[1]): int(sm[1]) + int(sm[2])] if ok and sm[0] else None,
+                biggest=(r[int(bg[1]): int(bg[1]) + int(bg[2])] + r[int(bg[3]): int(bg[3]) + int(bg[4])])
+                if ok and bg[0] else None))
+        return out
+
+
 _DEFAULT: dict[int, Codec] = {}
 
 

@@ -59,6 +59,7 @@ struct lsmgpu_ctx {
   DevBuf scan_tmp;
   DevBuf wsc;            // walk-scan-copy decode scratch (metadata, per-block triples)
   DevBuf wsc_tmp;        // its scan temporary storage
+  DevBuf open_tmp;       // batched table open: per-table scratch + scan temporary storage
   DevBuf wsc_carry;      // chunk carries ((kWscMaxChunks + 1) x 3 u64, [0..2] = 0)
   hipStream_t aux = nullptr;               // walk-scan-copy: the copy kernels' stream
   hipEvent_t wev[kWscMaxChunks + 1] = {};  // chunk c walked + scanned; [chunks] copies done
@@ -139,7 +140,7 @@ void lsmgpu_close(lsmgpu_ctx* c) {
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
   if (c->aux) (void)hipStreamSynchronize(c->aux);
   DevBuf* bufs[] = {&c->lb, &c->result, &c->flags, &c->scan_tmp, &c->wsc, &c->wsc_tmp,
-                    &c->wsc_carry, &c->s_data,
+                    &c->wsc_carry, &c->open_tmp, &c->s_data,
                     &c->s_off, &c->s_len, &c->s_kd, &c->s_ke, &c->s_vd, &c->s_ve, &c->s_view,
                     &c->s_bf, &c->s_bs, &c->s_a, &c->s_b, &c->s_c, &c->s_d};
   for (DevBuf* b : bufs) b->release();
@@ -612,6 +613,42 @@ int lsmgpu_encode_values(lsmgpu_ctx* c, const uint8_t* meta, const uint8_t* user
     HIPC(hipMemcpyAsync(vs_end, p.vs_end, n * 4, hipMemcpyDeviceToHost, c->stream));
   }
   HIPC(hipStreamSynchronize(c->stream));
+  return LSMGPU_OK;
+}
+
+// ------------------------------------------------------------------ batched table open
+int lsmgpu_open_tables_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t data_len,
+                             const uint64_t* d_sst_off, const uint64_t* d_sst_len,
+                             uint32_t ntables, const lsmgpu_tables* out, uint64_t* d_result) {
+  if (!c || !out || !d_result) return LSMGPU_ERR_ARG;
+  if (ntables && (!d_data || !d_sst_off || !d_sst_len)) return LSMGPU_ERR_ARG;
+  if (!out->nblk || !out->blk_base || !out->bloom_off || !out->bloom_len || !out->status ||
+      !out->smallest || !out->biggest)
+    return LSMGPU_ERR_ARG;
+  if (out->blk_cap && (!out->blk_off || !out->blk_len || !out->key_off || !out->key_len ||
+                       !out->order))
+    return LSMGPU_ERR_ARG;
+  if (out->blk_cap > 0xffffffffull) return LSMGPU_ERR_TOO_LARGE;
+  HIPC(hipSetDevice(c->device));
+  HIPC(hipMemsetAsync(d_result, 0, 8 * sizeof(uint64_t), c->stream));
+  if (ntables == 0) return LSMGPU_OK;
+  const size_t scratch = ((size_t)ntables * 8 + 255) / 256 * 256;
+  const size_t sbytes = open_scan_bytes(ntables);
+  if (scratch + sbytes > c->open_tmp.cap) {
+    HIPC(hipStreamSynchronize(c->stream));
+    HIPC(c->open_tmp.ensure(scratch + sbytes));
+  }
+  OpenParams p{};
+  p.data = d_data;
+  p.data_len = data_len;
+  p.sst_off = d_sst_off;
+  p.sst_len = d_sst_len;
+  p.ntables = ntables;
+  p.out = *out;
+  p.rpos = c->open_tmp.as<uint32_t>();
+  p.flags = p.rpos + ntables;
+  p.result = d_result;
+  HIPC(launch_open_tables(p, c->open_tmp.as<uint8_t>() + scratch, sbytes, c->stream));
   return LSMGPU_OK;
 }
 

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/lsmgpu.h"
+
 namespace lsmgpu {
 
 // Decode: one-wave workgroups over a persistent, fully resident grid, one SST data block per
@@ -72,6 +74,23 @@ struct ValuesParams {
   uint8_t* vs;
   uint32_t* vs_end;   // input: already holds the scanned end offsets
 };
+
+// Batched table open (open_tables.hip): per-table scratch rpos (restart array position) and
+// flags (error / unsorted bits), both ntables u32.
+struct OpenParams {
+  const uint8_t* data;
+  uint64_t data_len;
+  const uint64_t* sst_off;
+  const uint64_t* sst_len;
+  uint32_t ntables;
+  lsmgpu_tables out;
+  uint32_t* rpos;
+  uint32_t* flags;
+  uint64_t* result;
+};
+size_t open_scan_bytes(uint32_t ntables);
+hipError_t launch_open_tables(const OpenParams& p, void* scan_tmp, size_t scan_bytes,
+                              hipStream_t s);
 
 // launchers (return hipError_t)
 hipError_t launch_decode(const DecodeParams& p, uint32_t max_blk_len, int num_cus,

@@ -449,3 +449,114 @@ double sstref_decode_bench(const uint8_t* data, size_t data_len, const uint32_t*
   free(th); free(args);
   return secs;
 }
+
+/* ------------------------------------------------------------------ table/table.go OpenTable */
+
+static const uint8_t* g_sort_sst;   /* qsort context (single-threaded test oracle) */
+static const uint32_t* g_sort_koff;
+static const uint32_t* g_sort_klen;
+static int cmp_block_keys(const void* a, const void* b) {
+  const uint32_t i = *(const uint32_t*)a, j = *(const uint32_t*)b;
+  int c = sstref_compare_keys(g_sort_sst + g_sort_koff[i], g_sort_klen[i],
+                              g_sort_sst + g_sort_koff[j], g_sort_klen[j]);
+  if (c) return c;
+  return i < j ? -1 : (i > j ? 1 : 0); /* ties: SST order (documented divergence) */
+}
+
+int sstref_open_table(const uint8_t* sst, size_t len, uint32_t* blk_off, uint32_t* blk_len,
+                      uint32_t* key_off, uint32_t* key_len, uint32_t* order, size_t cap,
+                      sstref_table_info* info) {
+  memset(info, 0, sizeof(*info));
+  size_t nblk = 0, bo = 0, bl = 0;
+  int rc = sstref_parse_index(sst, len, blk_off, blk_len, cap, &nblk, &bo, &bl);
+  if (rc == -1) return info->status = SSTREF_TBL_BAD_TAIL;
+  info->nblk = (uint32_t)nblk;
+  if (rc == -2) return info->status = SSTREF_TBL_CAPACITY;
+  info->bloom_off = (uint32_t)bo;
+  info->bloom_len = (uint32_t)bl;
+  /* readIndex first headers and keys (table.go:219-256): t.read checks the whole file */
+  int plen_bad = 0, read_bad = 0;
+  for (size_t i = 0; i < nblk; i++) {
+    const size_t off = blk_off[i];
+    key_off[i] = 0;
+    key_len[i] = 0;
+    if (off + 10 > len) { read_bad = 1; continue; }           /* "While reading first header" */
+    const uint16_t plen = be16(sst + off), klen = be16(sst + off + 2);
+    if (plen != 0) { plen_bad = 1; continue; }                /* table.go:239 */
+    if (off + 10 + klen > len) { read_bad = 1; continue; }    /* "While reading first key" */
+    key_off[i] = (uint32_t)(off + 10);
+    key_len[i] = klen;
+  }
+  if (plen_bad) return info->status = SSTREF_TBL_FIRST_PLEN;
+  if (read_bad) return info->status = SSTREF_TBL_READ;
+  for (size_t i = 0; i < nblk; i++) order[i] = (uint32_t)i;
+  if (nblk >= 2) {                                            /* table.go:267 sort.Sort(byKey) */
+    for (size_t i = 0; i < nblk; i++)
+      if (key_len[i] <= 8) return info->status = SSTREF_TBL_KEY_LEN; /* y.go:85 */
+    g_sort_sst = sst;
+    g_sort_koff = key_off;
+    g_sort_klen = key_len;
+    qsort(order, nblk, sizeof(uint32_t), cmp_block_keys);
+  }
+  if (nblk == 0) return info->status = SSTREF_TBL_OK;         /* both iterators: io.EOF */
+  /* smallest: seekToFirst -> block order[0] SeekToFirst -> Init -> Next (iterator.go:81-84,112-135) */
+  {
+    const uint32_t b = order[0], off = blk_off[b], bl = blk_len[b];
+    if (bl >= 10) {
+      const uint16_t plen = be16(sst + off), klen = be16(sst + off + 2), vlen = be16(sst + off + 4);
+      if (!(klen == 0 && plen == 0) && 10u + klen + vlen <= bl) {
+        info->has_smallest = 1;
+        info->smallest_off = off + 10;
+        info->smallest_len = klen;
+      }
+    }
+  }
+  /* biggest: seekToLast -> block order[n-1].SeekToLast: Next until invalid, then Prev().
+   * Go's block slice is a window of the mmap'd file: reads past the block but inside the
+   * file (headers, keys, baseKey[:plen]) are legal and read the following bytes; only reads
+   * past the file panic (-> SSTREF_TBL_BIGGEST).  Bounds below are therefore `len`. */
+  {
+    const uint32_t b = order[nblk - 1], off = blk_off[b], bl = blk_len[b];
+    uint32_t pos = 0, last_prev = 0;                          /* itr.last: the zero header */
+    int have_base = 0, bad = 0;
+    for (;;) {                                                /* Next(), iterator.go:112-135 */
+      if (pos >= bl) break;                                   /* io.EOF */
+      if ((size_t)off + pos + 10 > len) { bad = 1; break; }   /* h.Decode past the file */
+      const uint16_t plen = be16(sst + off + pos), klen = be16(sst + off + pos + 2),
+                     vlen = be16(sst + off + pos + 4);
+      last_prev = be32(sst + off + pos + 6);
+      pos += 10;
+      if (klen == 0 && plen == 0) break;                      /* io.EOF */
+      if (!have_base) {
+        if (plen != 0) { bad = 1; break; }                    /* AssertTrue(h.plen == 0) */
+        if ((size_t)off + pos + klen > len) { bad = 1; break; }
+        have_base = 1;                                        /* baseKey = data[10:10+klen] */
+      }
+      if ((size_t)off + 10 + plen > len || (size_t)off + pos + klen > len) { bad = 1; break; }
+      pos += klen;                                            /* parseKV */
+      if (pos + vlen > bl) break;                             /* "Value exceeded": invalid */
+      pos += vlen;
+    }
+    if (!bad && last_prev != MAXU32) {                        /* Prev(), iterator.go:137-155 */
+      const uint32_t p = last_prev;
+      if (p >= bl || (size_t)off + p + 10 > len) {
+        bad = 1;                                              /* AssertTruef(pos < len) / Decode */
+      } else {
+        const uint16_t plen = be16(sst + off + p), klen = be16(sst + off + p + 2),
+                       vlen = be16(sst + off + p + 4);
+        const size_t base_cap = have_base ? len - (off + 10) : 0; /* cap(baseKey) */
+        if (plen > base_cap || (size_t)off + p + 10 + klen > len) {
+          bad = 1;
+        } else if ((uint64_t)p + 10 + klen + vlen <= bl) {    /* else parseKV error: invalid */
+          info->has_biggest = 1;
+          info->big_base_off = off + 10;
+          info->big_plen = plen;
+          info->big_diff_off = off + p + 10;
+          info->big_klen = klen;
+        }
+      }
+    }
+    if (bad) return info->status = SSTREF_TBL_BIGGEST;
+  }
+  return info->status = SSTREF_TBL_OK;
+}

@@ -107,6 +107,38 @@ double sstref_decode_bench(const uint8_t* data, size_t data_len, const uint32_t*
                            const uint32_t* blk_len, size_t nblk, int nthreads, int reps,
                            uint64_t* checksum);
 
+/* ---- table/table.go OpenTable index work (table.go:88-144 OpenTable, 177-269 readIndex) ----
+ * Per-table status; a Go panic / error becomes a code (priority: the first listed wins). */
+enum {
+  SSTREF_TBL_OK = 0,
+  SSTREF_TBL_BAD_TAIL = 1,    /* malformed tail (sstref_parse_index -1)                        */
+  SSTREF_TBL_FIRST_PLEN = 2,  /* table.go:239 AssertTruef(h.plen == 0): a panic                */
+  SSTREF_TBL_READ = 3,        /* table.go:226-237 t.read past the file: readIndex returns err  */
+  SSTREF_TBL_KEY_LEN = 4,     /* sort.Sort -> y.CompareKeys AssertTrue(len > 8): a panic       */
+  SSTREF_TBL_CAPACITY = 5,    /* more blocks than the caller's capacity                        */
+  SSTREF_TBL_BIGGEST = 6      /* SeekToLast/Prev would panic or read past the block; biggest nil */
+};
+typedef struct {
+  uint32_t nblk;
+  uint32_t bloom_off, bloom_len;
+  int32_t  status;
+  /* smallest = Rewind() of a forward iterator: first entry of block order[0] (iterator.go:201-217) */
+  int32_t  has_smallest;
+  uint32_t smallest_off, smallest_len;             /* table-relative key span (plen == 0)    */
+  /* biggest = Rewind() of a reversed iterator: block order[nblk-1].SeekToLast() ->
+   * walk forward until invalid, then Prev() to the last decoded header's `prev`
+   * (iterator.go:86-91,137-155); key = baseKey[:plen] ++ diff */
+  int32_t  has_biggest;
+  uint32_t big_base_off, big_plen, big_diff_off, big_klen;  /* table-relative */
+} sstref_table_info;
+/* blk_off/blk_len (table-relative, SST order), key_off/key_len (each block's first key, the
+ * blockIndex keys), order[i] = SST index of the i-th block of the sorted blockIndex
+ * (sort.Sort(byKey), table.go:267; equal keys keep SST order -- Go's sort is unstable).
+ * Returns info->status. */
+int sstref_open_table(const uint8_t* sst, size_t len, uint32_t* blk_off, uint32_t* blk_len,
+                      uint32_t* key_off, uint32_t* key_len, uint32_t* order, size_t cap,
+                      sstref_table_info* info);
+
 /* ---- y/y.go key helpers ---- */
 int sstref_compare_keys(const uint8_t* k1, size_t l1, const uint8_t* k2, size_t l2); /* y.go:84-90 */
 

@@ -20,6 +20,14 @@ class Totals(ctypes.Structure):
                 ("first_bad_block", c_int64), ("n_bad_blocks", c_uint64), ("overflow", c_int)]
 
 
+class TableInfo(ctypes.Structure):
+    _fields_ = [("nblk", c_uint32), ("bloom_off", c_uint32), ("bloom_len", c_uint32),
+                ("status", ctypes.c_int32), ("has_smallest", ctypes.c_int32),
+                ("smallest_off", c_uint32), ("smallest_len", c_uint32),
+                ("has_biggest", ctypes.c_int32), ("big_base_off", c_uint32), ("big_plen", c_uint32),
+                ("big_diff_off", c_uint32), ("big_klen", c_uint32)]
+
+
 _lib = None
 
 
@@ -66,6 +74,9 @@ def lib():
         L.sstref_decode_bench.restype = ctypes.c_double
         L.sstref_compare_keys.argtypes = [c_void_p, c_size_t, c_void_p, c_size_t]
         L.sstref_compare_keys.restype = c_int
+        L.sstref_open_table.argtypes = [c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p, c_size_t, POINTER(TableInfo)]
+        L.sstref_open_table.restype = c_int
         _lib = L
     return _lib
 
@@ -195,3 +206,31 @@ def decode_bench(data: np.ndarray, blk_off, blk_len, nthreads: int, reps: int):
 
 
 _ = (c_int64,)
+
+
+def open_table(sst: bytes, cap: int = 1 << 20) -> dict:
+    """OpenTable's index work (sstref_open_table; table.go:88-144,177-269): per-block
+    [off,len), first keys, sorted order, smallest / biggest (as bytes, or None)."""
+    a = _u8(sst)
+    off = np.zeros(cap, np.uint32)
+    ln = np.zeros(cap, np.uint32)
+    ko = np.zeros(cap, np.uint32)
+    kl = np.zeros(cap, np.uint32)
+    order = np.zeros(cap, np.uint32)
+    info = TableInfo()
+    lib().sstref_open_table(_p(a), a.size, _p(off), _p(ln), _p(ko), _p(kl), _p(order), cap,
+                            byref(info))
+    n = info.nblk if info.status != 5 else 0
+    raw = bytes(a)
+    smallest = raw[info.smallest_off: info.smallest_off + info.smallest_len] if info.has_smallest else None
+    biggest = None
+    if info.has_biggest:
+        biggest = (raw[info.big_base_off: info.big_base_off + info.big_plen] +
+                   raw[info.big_diff_off: info.big_diff_off + info.big_klen])
+    return dict(status=info.status, nblk=info.nblk, bloom_off=info.bloom_off,
+                bloom_len=info.bloom_len, blk_off=off[:n].copy(), blk_len=ln[:n].copy(),
+                key_off=ko[:n].copy(), key_len=kl[:n].copy(), order=order[:n].copy(),
+                smallest=smallest, biggest=biggest,
+                smallest_view=(info.has_smallest, info.smallest_off, info.smallest_len),
+                biggest_view=(info.has_biggest, info.big_base_off, info.big_plen,
+                              info.big_diff_off, info.big_klen))
