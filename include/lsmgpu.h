@@ -190,6 +190,43 @@ int lsmgpu_open_tables_async(lsmgpu_ctx* ctx, const uint8_t* d_data, uint64_t da
                              const uint64_t* d_sst_off, const uint64_t* d_sst_len,
                              uint32_t ntables, const lsmgpu_tables* out, uint64_t* d_result);
 
+/* ---- K-way merge of sorted runs --------------------------------------
+ * y.MergeIterator (y/iterator.go:74-202) as used by compactBuildTables (levels.go:239-258):
+ * run r = entries [run_first[r], run_first[r+1]) of one key / value stream in the layout
+ * lsmgpu_decode_blocks produces (a decode of all input tables in one batch: run_first =
+ * blk_first of each table's first block).  Output = the iterator's sequence: CompareKeys order,
+ * equal keys resolved to the lowest run index (`nice`), every later entry equal to the last
+ * emitted key dropped (y/iterator.go:159-184).  Values are the raw ValueStruct bytes
+ * (Value() + Builder.Add re-encode them identically when the uvarint is canonical).
+ * Runs must be in CompareKeys order (SSTs are) and keys longer than 8 B (CompareKeys asserts
+ * it): otherwise result[3] has LSMGPU_MERGE_UNSORTED / LSMGPU_MERGE_KEY_LEN and nothing is
+ * written.  All pointers are device pointers; asynchronous on the context's stream.
+ * d_result (8 u64): [0] entries out, [1] key bytes, [2] value bytes, [3] flags. */
+#define LSMGPU_MERGE_UNSORTED 1
+#define LSMGPU_MERGE_KEY_LEN 2
+#define LSMGPU_MERGE_CAPACITY 4
+typedef struct {
+  const uint8_t* key_data;
+  const uint32_t* key_end;   /* running end offsets over all runs (key i = [key_end[i-1], key_end[i])) */
+  const uint8_t* val_data;
+  const uint32_t* val_end;
+  const uint32_t* run_first; /* nruns + 1 entries, device */
+  uint32_t nruns;
+  uint64_t n;                /* run_first[nruns] */
+} lsmgpu_runs;
+typedef struct {
+  uint8_t* key_data;         /* may be NULL (keys not gathered) */
+  uint64_t key_cap;
+  uint32_t* key_end;
+  uint8_t* val_data;         /* may be NULL */
+  uint64_t val_cap;
+  uint32_t* val_end;
+  uint32_t* src;             /* may be NULL: input entry index of each output entry */
+  uint64_t ent_cap;
+} lsmgpu_merged;
+int lsmgpu_merge_runs_async(lsmgpu_ctx* ctx, const lsmgpu_runs* in, const lsmgpu_merged* out,
+                            uint64_t* d_result);
+
 #ifdef __cplusplus
 }
 #endif

@@ -48,6 +48,7 @@ EXPORTED_SYMBOLS = (
     "lsmgpu_abi_version",
     "lsmgpu_parse_index",
     "lsmgpu_open_tables_async",
+    "lsmgpu_merge_runs_async",
     "lsmgpu_decode_blocks",
     "lsmgpu_decode_blocks_async",
     "lsmgpu_encode_blocks",
@@ -94,6 +95,20 @@ class Tables(ctypes.Structure):
         ("order", c_void_p),
         ("blk_cap", c_uint64),
     ]
+
+
+class Runs(ctypes.Structure):
+    """lsmgpu_runs (include/lsmgpu.h): sorted runs of one key / value stream, device pointers."""
+    _fields_ = [("key_data", c_void_p), ("key_end", c_void_p), ("val_data", c_void_p),
+                ("val_end", c_void_p), ("run_first", c_void_p), ("nruns", c_uint32),
+                ("n", c_uint64)]
+
+
+class Merged(ctypes.Structure):
+    """lsmgpu_merged (include/lsmgpu.h): merge output, device pointers."""
+    _fields_ = [("key_data", c_void_p), ("key_cap", c_uint64), ("key_end", c_void_p),
+                ("val_data", c_void_p), ("val_cap", c_uint64), ("val_end", c_void_p),
+                ("src", c_void_p), ("ent_cap", c_uint64)]
 
 
 class LsmgpuError(RuntimeError):
@@ -163,6 +178,8 @@ def _load() -> ctypes.CDLL:
     lib.lsmgpu_open_tables_async.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p,
                                              c_uint32, POINTER(Tables), c_void_p]
     lib.lsmgpu_open_tables_async.restype = c_int
+    lib.lsmgpu_merge_runs_async.argtypes = [c_void_p, POINTER(Runs), POINTER(Merged), c_void_p]
+    lib.lsmgpu_merge_runs_async.restype = c_int
     return lib
 
 

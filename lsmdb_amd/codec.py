@@ -337,6 +337,51 @@ class Codec:
         return out
 
 
+    # -- k-way merge (MergeIterator, y/iterator.go:74-202)
+    def merge_device(self, key_data, key_end, val_data, val_end, run_first, n: int,
+                     gather: bool = True) -> dict:
+        """Sorted runs [run_first[r], run_first[r+1]) of one device SoA stream -> merged SoA
+        (asynchronous).  Returns device tensors key_data/key_end/val_data/val_end/src/result."""
+        import torch
+        dev = key_end.device
+        kcap = int(key_data.numel()) if gather else 0
+        vcap = int(val_data.numel()) if gather and val_data is not None else 0
+        o = dict(key_end=torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+                 val_end=torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+                 src=torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+                 key_data=torch.empty(max(kcap, 16), dtype=torch.uint8, device=dev) if gather else None,
+                 val_data=torch.empty(max(vcap, 16), dtype=torch.uint8, device=dev) if vcap else None,
+                 result=torch.zeros(8, dtype=torch.int64, device=dev))
+        runs = _lib.Runs(_ptr(key_data), _ptr(key_end), _ptr(val_data), _ptr(val_end),
+                         _ptr(run_first), run_first.numel() - 1, n)
+        out = _lib.Merged(_ptr(o["key_data"]), kcap, _ptr(o["key_end"]), _ptr(o["val_data"]),
+                          vcap, _ptr(o["val_end"]), _ptr(o["src"]), max(n, 1))
+        check(lib().lsmgpu_merge_runs_async(self._ctx, byref(runs), byref(out), _ptr(o["result"])),
+              "merge_runs_async")
+        return o
+
+    def merge_host(self, key_data, key_end, val_data, val_end, run_first):
+        """Host arrays in, host arrays out: (keys bytes, key_end, vals bytes, val_end, src,
+        flags)."""
+        import torch
+        ke = np.ascontiguousarray(key_end, dtype=np.uint32)
+        ve = np.ascontiguousarray(val_end, dtype=np.uint32)
+        rf = np.ascontiguousarray(run_first, dtype=np.uint32)
+        n = int(rf[-1])
+        t = lambda a, dt: torch.from_numpy(np.array(a, copy=True).view(dt)).to(self.device)
+        kd = t(np.frombuffer(bytes(key_data) + b"\0" * 16, np.uint8), np.uint8)
+        vd = t(np.frombuffer(bytes(val_data) + b"\0" * 16, np.uint8), np.uint8)
+        o = self.merge_device(kd, t(ke, np.int32), vd, t(ve, np.int32), t(rf, np.int32), n)
+        self.synchronize()
+        r = o["result"].cpu().numpy()
+        m, kb, vb = int(r[0]), int(r[1]), int(r[2])
+        return (o["key_data"][:kb].cpu().numpy().tobytes(),
+                o["key_end"][:m].cpu().numpy().view(np.uint32),
+                o["val_data"][:vb].cpu().numpy().tobytes(),
+                o["val_end"][:m].cpu().numpy().view(np.uint32),
+                o["src"][:m].cpu().numpy().view(np.uint32), int(r[3]))
+
+
 _DEFAULT: dict[int, Codec] = {}
 
 

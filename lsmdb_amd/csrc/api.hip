@@ -60,6 +60,7 @@ struct lsmgpu_ctx {
   DevBuf wsc;            // walk-scan-copy decode scratch (metadata, per-block triples)
   DevBuf wsc_tmp;        // its scan temporary storage
   DevBuf open_tmp;       // batched table open: per-table scratch + scan temporary storage
+  DevBuf merge_tmp;      // k-way merge: permutation, triples, scan, flags, scan storage
   DevBuf wsc_carry;      // chunk carries ((kWscMaxChunks + 1) x 3 u64, [0..2] = 0)
   hipStream_t aux = nullptr;               // walk-scan-copy: the copy kernels' stream
   hipEvent_t wev[kWscMaxChunks + 1] = {};  // chunk c walked + scanned; [chunks] copies done
@@ -140,7 +141,7 @@ void lsmgpu_close(lsmgpu_ctx* c) {
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
   if (c->aux) (void)hipStreamSynchronize(c->aux);
   DevBuf* bufs[] = {&c->lb, &c->result, &c->flags, &c->scan_tmp, &c->wsc, &c->wsc_tmp,
-                    &c->wsc_carry, &c->open_tmp, &c->s_data,
+                    &c->wsc_carry, &c->open_tmp, &c->merge_tmp, &c->s_data,
                     &c->s_off, &c->s_len, &c->s_kd, &c->s_ke, &c->s_vd, &c->s_ve, &c->s_view,
                     &c->s_bf, &c->s_bs, &c->s_a, &c->s_b, &c->s_c, &c->s_d};
   for (DevBuf* b : bufs) b->release();
@@ -649,6 +650,51 @@ int lsmgpu_open_tables_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t data
   p.flags = p.rpos + ntables;
   p.result = d_result;
   HIPC(launch_open_tables(p, c->open_tmp.as<uint8_t>() + scratch, sbytes, c->stream));
+  return LSMGPU_OK;
+}
+
+// ------------------------------------------------------------------ k-way merge
+int lsmgpu_merge_runs_async(lsmgpu_ctx* c, const lsmgpu_runs* in, const lsmgpu_merged* out,
+                            uint64_t* d_result) {
+  if (!c || !in || !out || !d_result) return LSMGPU_ERR_ARG;
+  if (in->n > 0xfffffffeull) return LSMGPU_ERR_TOO_LARGE;
+  if (in->n && (!in->key_data || !in->key_end || !in->val_end || !in->run_first || in->nruns == 0))
+    return LSMGPU_ERR_ARG;
+  if (out->val_data && !in->val_data) return LSMGPU_ERR_ARG;
+  HIPC(hipSetDevice(c->device));
+  HIPC(hipMemsetAsync(d_result, 0, 8 * sizeof(uint64_t), c->stream));
+  const uint32_t n = (uint32_t)in->n;
+  auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+  const size_t dst_b = al((size_t)n * 4 + 4), tri_b = al((size_t)n * 24 + 24), flg_b = 256;
+  const size_t sbytes = merge_scan_bytes(n ? n : 1);
+  const size_t need = dst_b + 2 * tri_b + flg_b + sbytes;
+  if (need > c->merge_tmp.cap) {
+    HIPC(hipStreamSynchronize(c->stream));
+    HIPC(c->merge_tmp.ensure(need));
+  }
+  uint8_t* w = c->merge_tmp.as<uint8_t>();
+  MergeParams p{};
+  p.kd = in->key_data;
+  p.ke = in->key_end;
+  p.vd = in->val_data;
+  p.ve = in->val_end;
+  p.run_first = in->run_first;
+  p.nruns = in->nruns;
+  p.n = n;
+  p.dst = reinterpret_cast<uint32_t*>(w);
+  p.tri = reinterpret_cast<uint64_t*>(w + dst_b);
+  p.base = reinterpret_cast<uint64_t*>(w + dst_b + tri_b);
+  p.flags = reinterpret_cast<uint32_t*>(w + dst_b + 2 * tri_b);
+  p.okd = out->key_data;
+  p.key_cap = out->key_cap;
+  p.oke = out->key_end;
+  p.ovd = out->val_data;
+  p.val_cap = out->val_cap;
+  p.ove = out->val_end;
+  p.osrc = out->src;
+  p.ent_cap = out->ent_cap;
+  p.result = d_result;
+  HIPC(launch_merge(p, w + dst_b + 2 * tri_b + flg_b, sbytes, c->stream));
   return LSMGPU_OK;
 }
 

@@ -83,6 +83,37 @@ __device__ __forceinline__ void set_byte(uint4& v, int i, uint32_t b) {
   }
 }
 
+// A stream of `len` bytes copied global -> global (any alignment) as independent pieces:
+// 16-B pieces, the last one overlapping back inside the stream; below 16 B two overlapping
+// 8-B or 4-B pieces; below 4 B single bytes.  No piece touches a byte outside the stream, so
+// neighbouring streams can be written concurrently.  pieces16 = the piece count, copy_piece16
+// copies piece q.
+__device__ __forceinline__ uint32_t pieces16(uint32_t len) {
+  return len >= 16 ? (len + 15) >> 4 : (len >= 4 ? 2u : len);
+}
+__device__ __forceinline__ void copy_piece16(uint8_t* dst, const uint8_t* src, uint32_t len,
+                                          uint32_t q) {
+  if (len >= 16) {
+    const uint32_t o = min(16 * q, len - 16);
+    uint4 v;
+    __builtin_memcpy(&v, src + o, 16);
+    __builtin_memcpy(dst + o, &v, 16);
+  } else if (len >= 8) {
+    const uint32_t o = q ? len - 8 : 0;
+    uint2 v;
+    __builtin_memcpy(&v, src + o, 8);
+    __builtin_memcpy(dst + o, &v, 8);
+  } else if (len >= 4) {
+    const uint32_t o = q ? len - 4 : 0;
+    uint32_t v;
+    __builtin_memcpy(&v, src + o, 4);
+    __builtin_memcpy(dst + o, &v, 4);
+  } else {
+    dst[q] = src[q];
+  }
+}
+
+
 // Copies [src, src+n) of global memory (any alignment, n = multiple-of-16 region base given)
 // into LDS as 16-B chunks: lds[16c .. 16c+16) = global[a0+16c ..], a0 = src & ~15.
 // Bytes past `limit` (end of the readable global buffer) are never read (zero-filled).

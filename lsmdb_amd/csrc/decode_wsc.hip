@@ -105,64 +105,6 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   p.wstatus[b] = st;
 }
 
-// Copy `len` bytes from src to dst (both global, any alignment) with the J lanes of a group:
-// lane j writes pieces j, j + J, ...; 16-B pieces, the last overlapping back inside the range,
-// or two overlapping 8/4-B pieces below 16 B, bytes below 4 B.
-__device__ __forceinline__ void group_copy(uint8_t* dst, const uint8_t* src, uint32_t len,
-                                           uint32_t j, uint32_t J) {
-  if (len >= 16) {
-    const uint32_t np = (len + 15) >> 4;
-    for (uint32_t q = j; q < np; q += J) {
-      const uint32_t o = min(16 * q, len - 16);
-      uint4 v;
-      __builtin_memcpy(&v, src + o, 16);
-      __builtin_memcpy(dst + o, &v, 16);
-    }
-  } else if (len >= 8) {
-    if (j < 2) {
-      const uint32_t o = j ? len - 8 : 0;
-      uint2 v;
-      __builtin_memcpy(&v, src + o, 8);
-      __builtin_memcpy(dst + o, &v, 8);
-    }
-  } else if (len >= 4) {
-    if (j < 2) {
-      const uint32_t o = j ? len - 4 : 0;
-      uint32_t v;
-      __builtin_memcpy(&v, src + o, 4);
-      __builtin_memcpy(dst + o, &v, 4);
-    }
-  } else if (j < len) {
-    dst[j] = src[j];
-  }
-}
-
-// Pieces of a stream of `len` bytes (see group_copy) and piece q of it.
-__device__ __forceinline__ uint32_t n_pieces16(uint32_t len) {
-  return len >= 16 ? (len + 15) >> 4 : (len >= 4 ? 2u : len);
-}
-__device__ __forceinline__ void piece_copy(uint8_t* dst, const uint8_t* src, uint32_t len,
-                                           uint32_t q) {
-  if (len >= 16) {
-    const uint32_t o = min(16 * q, len - 16);
-    uint4 v;
-    __builtin_memcpy(&v, src + o, 16);
-    __builtin_memcpy(dst + o, &v, 16);
-  } else if (len >= 8) {
-    const uint32_t o = q ? len - 8 : 0;
-    uint2 v;
-    __builtin_memcpy(&v, src + o, 8);
-    __builtin_memcpy(dst + o, &v, 8);
-  } else if (len >= 4) {
-    const uint32_t o = q ? len - 4 : 0;
-    uint32_t v;
-    __builtin_memcpy(&v, src + o, 4);
-    __builtin_memcpy(dst + o, &v, 4);
-  } else {
-    dst[q] = src[q];
-  }
-}
-
 // The entries of one block: J lanes per entry; an entry's pieces are [key pieces | value
 // pieces] (16 B, the last overlapping back inside its stream, or two overlapping 8/4/2/1-B
 // pieces below 16 B) and lane j takes pieces j, j + J, ...  G entry groups per pass, all
@@ -192,8 +134,8 @@ __device__ __forceinline__ void copy_entries(const DecodeParams& p, const uint2*
       const uint32_t plen = ko1 - ko[i] - kl[i];
       on[i] = e < n;
       any_plen = any_plen || (on[i] && plen != 0);
-      kp[i] = plen ? 0u : n_pieces16(kl[i]);  // prefix-compressed keys: bytewise pass below
-      np[i] = kp[i] + n_pieces16(vl[i]);
+      kp[i] = plen ? 0u : pieces16(kl[i]);  // prefix-compressed keys: bytewise pass below
+      np[i] = kp[i] + pieces16(vl[i]);
       if (on[i] && j == 0) {
         if (mat) {
           if (p.key_end) p.key_end[en + e] = (uint32_t)(ek + ko1);
@@ -214,7 +156,7 @@ __device__ __forceinline__ void copy_entries(const DecodeParams& p, const uint2*
         uint8_t* dst = key ? kbase : vbase;
         if (!dst) continue;
         const uint32_t s0 = key ? hp[i] + 10 : hp[i] + 10 + kl[i];
-        piece_copy(dst + (key ? ko[i] : vo[i]), blk + s0, len, key ? q : q - kp[i]);
+        copy_piece16(dst + (key ? ko[i] : vo[i]), blk + s0, len, key ? q : q - kp[i]);
       }
     }
   }
@@ -522,8 +464,8 @@ __global__ void __launch_bounds__(64) tile_decode_kernel(DecodeParams p) {
       // stored key bytes: the output key less its shared prefix (prefix-compressed tiles only)
       ks[i] = has_plen ? kl[i] - LdsSrc{slots + blk * kTileSlot, shb}.hdr(hp).plen : kl[i];
       on[i] = e < nt;
-      kp[i] = has_plen ? 0u : n_pieces16(kl[i]);  // prefix-compressed tiles: bytewise below
-      np[i] = kp[i] + n_pieces16(vl[i]);
+      kp[i] = has_plen ? 0u : pieces16(kl[i]);  // prefix-compressed tiles: bytewise below
+      np[i] = kp[i] + pieces16(vl[i]);
       if (on[i] && j == 0) {
         if (mat) {
           if (p.key_end) p.key_end[en + e] = (uint32_t)(ek + ko[i] + kl[i]);
@@ -542,7 +484,7 @@ __global__ void __launch_bounds__(64) tile_decode_kernel(DecodeParams p) {
         uint8_t* dst = key ? kbase : vbase;
         if (!dst) continue;
         const uint32_t len = key ? kl[i] : vl[i];
-        piece_copy(dst + (key ? ko[i] : vo[i]), p.data + (key ? src[i] : src[i] + ks[i]), len,
+        copy_piece16(dst + (key ? ko[i] : vo[i]), p.data + (key ? src[i] : src[i] + ks[i]), len,
                    key ? q : q - kp[i]);
       }
     }

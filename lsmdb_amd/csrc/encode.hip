@@ -53,32 +53,6 @@ __device__ __forceinline__ void store_header(uint8_t* d, uint32_t klen, uint32_t
   __builtin_memcpy(d + 8, &lo, 2);
 }
 
-// Pieces of a stream of `len` bytes and piece q of it (see the header comment).
-__device__ __forceinline__ uint32_t enc_pieces(uint32_t len) {
-  return len >= 16 ? (len + 15) >> 4 : (len >= 4 ? 2u : len);
-}
-__device__ __forceinline__ void enc_piece(uint8_t* dst, const uint8_t* src, uint32_t len,
-                                          uint32_t q) {
-  if (len >= 16) {
-    const uint32_t o = min(16 * q, len - 16);
-    uint4 v;
-    __builtin_memcpy(&v, src + o, 16);
-    __builtin_memcpy(dst + o, &v, 16);
-  } else if (len >= 8) {
-    const uint32_t o = q ? len - 8 : 0;
-    uint2 v;
-    __builtin_memcpy(&v, src + o, 8);
-    __builtin_memcpy(dst + o, &v, 8);
-  } else if (len >= 4) {
-    const uint32_t o = q ? len - 4 : 0;
-    uint32_t v;
-    __builtin_memcpy(&v, src + o, 4);
-    __builtin_memcpy(dst + o, &v, 4);
-  } else {
-    dst[q] = src[q];
-  }
-}
-
 template <uint32_t J, uint32_t G>
 __global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
   constexpr uint32_t EPP = kWave / J;      // entries per group pass; G group passes per loop
@@ -133,8 +107,8 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
         if (kl64 <= 8 || kl64 > 0xffff) bad |= 1;  // ParseKey needs len(key) > 8 (y.go:93-100)
         if (vl64 > 0xffff) bad |= 2;                // header vlen is a uint16
       }
-      kp[i] = enc_pieces(klen[i]);
-      np[i] = on[i] ? kp[i] + enc_pieces(vlen[i]) : 0u;
+      kp[i] = pieces16(klen[i]);
+      np[i] = on[i] ? kp[i] + pieces16(vlen[i]) : 0u;
     }
     if (e0 == 0) bs = readlane(pos[0], 0);
 #pragma unroll
@@ -160,7 +134,7 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
     for (uint32_t i = 0; i < G; i++) {
       for (uint32_t q = j; q < np[i]; q += J) {  // one (non-divergent) copy per piece
         const bool key = q < kp[i];
-        enc_piece(p.out + pos[i] + 10 + (key ? 0u : klen[i]), key ? p.keys + ks[i] : p.vs + vs0[i],
+        copy_piece16(p.out + pos[i] + 10 + (key ? 0u : klen[i]), key ? p.keys + ks[i] : p.vs + vs0[i],
                   key ? klen[i] : vlen[i], key ? q : q - kp[i]);
       }
     }

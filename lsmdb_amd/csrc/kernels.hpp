@@ -92,6 +92,32 @@ size_t open_scan_bytes(uint32_t ntables);
 hipError_t launch_open_tables(const OpenParams& p, void* scan_tmp, size_t scan_bytes,
                               hipStream_t s);
 
+// K-way merge (merge.hip): MergeIterator over nruns sorted runs of one key/value stream.
+struct MergeParams {
+  const uint8_t* kd;
+  const uint32_t* ke;
+  const uint8_t* vd;
+  const uint32_t* ve;
+  const uint32_t* run_first;  // nruns + 1
+  uint32_t nruns;
+  uint32_t n;                 // entries (run_first[nruns])
+  uint32_t* dst;              // scratch: merged position -> entry
+  uint64_t* tri;              // scratch: n x {keep, key bytes, value bytes}
+  uint64_t* base;             // scratch: their exclusive scan
+  uint32_t* flags;            // scratch: [0] input errors, [1] capacity
+  uint8_t* okd;
+  uint64_t key_cap;
+  uint32_t* oke;
+  uint8_t* ovd;
+  uint64_t val_cap;
+  uint32_t* ove;
+  uint32_t* osrc;
+  uint64_t ent_cap;
+  uint64_t* result;
+};
+size_t merge_scan_bytes(uint32_t n);
+hipError_t launch_merge(const MergeParams& p, void* scan_tmp, size_t scan_bytes, hipStream_t s);
+
 // launchers (return hipError_t)
 hipError_t launch_decode(const DecodeParams& p, uint32_t max_blk_len, int num_cus,
                          hipStream_t s, uint64_t* waves_launched);

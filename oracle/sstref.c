@@ -560,3 +560,46 @@ int sstref_open_table(const uint8_t* sst, size_t len, uint32_t* blk_off, uint32_
   }
   return info->status = SSTREF_TBL_OK;
 }
+
+/* ------------------------------------------------------------------ y/iterator.go MergeIterator */
+
+static inline const uint8_t* key_at(const uint8_t* kd, const uint32_t* ke, uint32_t i, uint32_t* len) {
+  const uint32_t s = i ? ke[i - 1] : 0;
+  *len = ke[i] - s;
+  return kd + s;
+}
+
+size_t sstref_merge(const uint8_t* kd, const uint32_t* ke, const uint32_t* run_first,
+                    size_t nruns, uint32_t* out_src, size_t cap) {
+  uint32_t* cur = (uint32_t*)malloc((nruns + 1) * sizeof(uint32_t));
+  for (size_t r = 0; r < nruns; r++) cur[r] = run_first[r];
+  size_t n = 0;
+  int have_last = 0;
+  uint32_t last = 0;
+  for (;;) {
+    /* the heap top: least valid head by (CompareKeys, nice)  (elemHeap.Less, y/iterator.go:82-93) */
+    long best = -1;
+    for (size_t r = 0; r < nruns; r++) {
+      if (cur[r] >= run_first[r + 1]) continue; /* !Valid(): popped (y/iterator.go:166-169) */
+      if (best < 0) { best = (long)r; continue; }
+      uint32_t la, lb;
+      const uint8_t* a = key_at(kd, ke, cur[r], &la);
+      const uint8_t* b = key_at(kd, ke, cur[best], &lb);
+      if (sstref_compare_keys(a, la, b, lb) < 0) best = (long)r; /* ties: lower nice (r) stays */
+    }
+    if (best < 0) break;
+    const uint32_t i = cur[best]++;
+    if (have_last) { /* Next(): skip heads equal to curKey (bytes.Equal, y/iterator.go:172-181) */
+      uint32_t la, lb;
+      const uint8_t* a = key_at(kd, ke, i, &la);
+      const uint8_t* b = key_at(kd, ke, last, &lb);
+      if (la == lb && memcmp(a, b, la) == 0) continue;
+    }
+    if (n >= cap) { free(cur); return (size_t)-1; }
+    out_src[n++] = i;
+    last = i;
+    have_last = 1;
+  }
+  free(cur);
+  return n;
+}

@@ -139,6 +139,15 @@ int sstref_open_table(const uint8_t* sst, size_t len, uint32_t* blk_off, uint32_
                       uint32_t* key_off, uint32_t* key_len, uint32_t* order, size_t cap,
                       sstref_table_info* info);
 
+/* ---- y/iterator.go MergeIterator (y/iterator.go:74-202) ----
+ * nruns iterators over entries [run_first[r], run_first[r+1]) of one key stream (key i =
+ * kd[ke[i-1]:ke[i]]).  The heap's top is always the least head under elemHeap.Less (CompareKeys,
+ * then lower nice = run index); Next() drops every head equal to the last emitted key
+ * (storeKey/curKey).  out_src[i] = entry index of the i-th output.  Returns the output count
+ * (or (size_t)-1 if cap is too small). */
+size_t sstref_merge(const uint8_t* kd, const uint32_t* ke, const uint32_t* run_first,
+                    size_t nruns, uint32_t* out_src, size_t cap);
+
 /* ---- y/y.go key helpers ---- */
 int sstref_compare_keys(const uint8_t* k1, size_t l1, const uint8_t* k2, size_t l2); /* y.go:84-90 */
 

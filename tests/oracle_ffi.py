@@ -77,6 +77,8 @@ def lib():
         L.sstref_open_table.argtypes = [c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_size_t, POINTER(TableInfo)]
         L.sstref_open_table.restype = c_int
+        L.sstref_merge.argtypes = [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t]
+        L.sstref_merge.restype = c_size_t
         _lib = L
     return _lib
 
@@ -234,3 +236,14 @@ def open_table(sst: bytes, cap: int = 1 << 20) -> dict:
                 smallest_view=(info.has_smallest, info.smallest_off, info.smallest_len),
                 biggest_view=(info.has_biggest, info.big_base_off, info.big_plen,
                               info.big_diff_off, info.big_klen))
+
+
+def merge(key_data, key_end, run_first) -> np.ndarray:
+    """MergeIterator order (sstref_merge): source entry index of each output entry."""
+    kd = _u8(key_data) if len(key_data) else np.zeros(1, np.uint8)
+    ke = np.ascontiguousarray(key_end, dtype=np.uint32)
+    rf = np.ascontiguousarray(run_first, dtype=np.uint32)
+    out = np.zeros(max(ke.size, 1), np.uint32)
+    n = lib().sstref_merge(_p(kd), _p(ke), _p(rf), rf.size - 1, _p(out), out.size)
+    assert n != ctypes.c_size_t(-1).value
+    return out[:n].copy()
