@@ -666,8 +666,10 @@ int lsmgpu_merge_runs_async(lsmgpu_ctx* c, const lsmgpu_runs* in, const lsmgpu_m
   const uint32_t n = (uint32_t)in->n;
   auto al = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t dst_b = al((size_t)n * 4 + 4), tri_b = al((size_t)n * 24 + 24), flg_b = 256;
+  const size_t tb_b = al(((size_t)in->nruns + 1) * 4);
+  const size_t spl_b = al(((size_t)n / 256 + in->nruns) * in->nruns * 4 + 4);
   const size_t sbytes = merge_scan_bytes(n ? n : 1);
-  const size_t need = dst_b + 2 * tri_b + flg_b + sbytes;
+  const size_t need = dst_b + 2 * tri_b + flg_b + tb_b + spl_b + sbytes;
   if (need > c->merge_tmp.cap) {
     HIPC(hipStreamSynchronize(c->stream));
     HIPC(c->merge_tmp.ensure(need));
@@ -685,6 +687,8 @@ int lsmgpu_merge_runs_async(lsmgpu_ctx* c, const lsmgpu_runs* in, const lsmgpu_m
   p.tri = reinterpret_cast<uint64_t*>(w + dst_b);
   p.base = reinterpret_cast<uint64_t*>(w + dst_b + tri_b);
   p.flags = reinterpret_cast<uint32_t*>(w + dst_b + 2 * tri_b);
+  p.tile_base = reinterpret_cast<uint32_t*>(w + dst_b + 2 * tri_b + flg_b);
+  p.spl = reinterpret_cast<uint32_t*>(w + dst_b + 2 * tri_b + flg_b + tb_b);
   p.okd = out->key_data;
   p.key_cap = out->key_cap;
   p.oke = out->key_end;
@@ -694,7 +698,7 @@ int lsmgpu_merge_runs_async(lsmgpu_ctx* c, const lsmgpu_runs* in, const lsmgpu_m
   p.osrc = out->src;
   p.ent_cap = out->ent_cap;
   p.result = d_result;
-  HIPC(launch_merge(p, w + dst_b + 2 * tri_b + flg_b, sbytes, c->stream));
+  HIPC(launch_merge(p, w + dst_b + 2 * tri_b + flg_b + tb_b + spl_b, sbytes, c->stream));
   return LSMGPU_OK;
 }
 

@@ -83,6 +83,29 @@ __device__ __forceinline__ void set_byte(uint4& v, int i, uint32_t b) {
   }
 }
 
+// bytes.Compare on global memory, 8-B big-endian words at a time (unaligned loads); the tail
+// bytewise.  Returns -1 / 0 / 1.
+__device__ __forceinline__ int bytes_compare(const uint8_t* a, uint32_t la, const uint8_t* b,
+                                             uint32_t lb) {
+  const uint32_t n = la < lb ? la : lb;
+  uint32_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t x, y;
+    __builtin_memcpy(&x, a + i, 8);
+    __builtin_memcpy(&y, b + i, 8);
+    if (x != y) return __builtin_bswap64(x) < __builtin_bswap64(y) ? -1 : 1;
+  }
+  for (; i < n; i++)
+    if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
+  return la == lb ? 0 : (la < lb ? -1 : 1);
+}
+// y.CompareKeys (y/y.go:84-90) for keys longer than 8 B: the user key, then the 8-B suffix
+__device__ __forceinline__ int compare_keys(const uint8_t* a, uint32_t la, const uint8_t* b,
+                                            uint32_t lb) {
+  const int c = bytes_compare(a, la - 8, b, lb - 8);
+  return c ? c : bytes_compare(a + la - 8, 8, b + lb - 8, 8);
+}
+
 // A stream of `len` bytes copied global -> global (any alignment) as independent pieces:
 // 16-B pieces, the last one overlapping back inside the stream; below 16 B two overlapping
 // 8-B or 4-B pieces; below 4 B single bytes.  No piece touches a byte outside the stream, so

@@ -105,6 +105,8 @@ struct MergeParams {
   uint64_t* tri;              // scratch: n x {keep, key bytes, value bytes}
   uint64_t* base;             // scratch: their exclusive scan
   uint32_t* flags;            // scratch: [0] input errors, [1] capacity
+  uint32_t* tile_base;        // scratch: nruns + 1
+  uint32_t* spl;              // scratch: (n / 256 + nruns) x nruns splitter ranks
   uint8_t* okd;
   uint64_t key_cap;
   uint32_t* oke;

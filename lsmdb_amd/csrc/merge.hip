@@ -7,10 +7,13 @@
 // runs (SSTs are) that is: the runs' stable merge under (CompareKeys, run), keeping the first
 // entry of each group of equal keys.  Computed without a heap, every entry in parallel:
 //   check  (lane = entry)   runs in CompareKeys order? keys > 8 B (CompareKeys asserts it)?
+//   split  (lane = tile x run) for the first entry of every 256-entry tile of a run, its rank
+//                           in every other run (full binary search)
 //   rank   (lane = entry)   merged position = own index in its run + for every other run the
-//                           number of entries that precede it: binary search, upper bound for
-//                           lower-index runs (equal keys of a lower nice come first), lower
-//                           bound for higher-index runs
+//                           number of entries that precede it: binary search between the
+//                           tile's splitters (ranks are monotone in a sorted run), upper bound
+//                           for lower-index runs (equal keys of a lower nice come first),
+//                           lower bound for higher-index runs
 //   keep   (lane = merged position)  first of its equal-key group (bytes.Equal with the
 //                           predecessor, y/iterator.go:172-181)
 //   scan   (rocPRIM)        output entry index, key and value byte offsets of the kept entries
@@ -27,6 +30,7 @@ namespace lsmgpu {
 namespace {
 
 constexpr uint32_t M_UNSORTED = 1, M_KEY_LEN = 2, M_CAPACITY = 4;
+constexpr uint32_t kMergeTile = 256;  // entries per splitter tile
 
 struct MTri {
   uint64_t n, k, v;
@@ -41,17 +45,6 @@ __device__ __forceinline__ const uint8_t* key_of(const MergeParams& p, uint32_t 
   const uint32_t s = i ? p.ke[i - 1] : 0u;
   len = p.ke[i] - s;
   return p.kd + s;
-}
-
-// y.CompareKeys (y.go:84-90) on keys of > 8 bytes: user key, then the 8-B timestamp suffix
-__device__ int cmp_keys(const uint8_t* a, uint32_t la, const uint8_t* b, uint32_t lb) {
-  const uint32_t ua = la - 8, ub = lb - 8, n = ua < ub ? ua : ub;
-  for (uint32_t i = 0; i < n; i++)
-    if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
-  if (ua != ub) return ua < ub ? -1 : 1;
-  for (uint32_t i = 0; i < 8; i++)
-    if (a[ua + i] != b[ub + i]) return a[ua + i] < b[ub + i] ? -1 : 1;
-  return 0;
 }
 
 __device__ __forceinline__ uint32_t run_of(const MergeParams& p, uint32_t i) {
@@ -78,31 +71,68 @@ __global__ void merge_check_kernel(MergeParams p) {
     if (i > p.run_first[r]) {
       uint32_t lp;
       const uint8_t* kp = key_of(p, i - 1, lp);
-      if (lp > 8 && cmp_keys(kp, lp, ki, li) > 0) fl = M_UNSORTED;
+      if (lp > 8 && compare_keys(kp, lp, ki, li) > 0) fl = M_UNSORTED;
     }
   }
   if (fl) atomicOr(p.flags, fl);
+}
+
+// Entries of run s that precede key x of run r (key < x, or == x with s < r: lower nice
+// first), searched in [lo, hi) of run s.
+__device__ __forceinline__ uint32_t rank_in(const MergeParams& p, uint32_t s, uint32_t r,
+                                            const uint8_t* kx, uint32_t lx, uint32_t lo,
+                                            uint32_t hi) {
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    uint32_t lm;
+    const uint8_t* km = key_of(p, mid, lm);
+    const int c = compare_keys(km, lm, kx, lx);
+    if (c < 0 || (c == 0 && s < r)) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// tile_base[r] = first tile of run r (tiles of kMergeTile entries never span runs)
+__global__ void merge_tiles_kernel(MergeParams p) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint32_t t = 0;
+  for (uint32_t r = 0; r < p.nruns; r++) {
+    p.tile_base[r] = t;
+    t += (p.run_first[r + 1] - p.run_first[r] + kMergeTile - 1) / kMergeTile;
+  }
+  p.tile_base[p.nruns] = t;
+}
+
+// Splitters: for the first entry of every tile, its absolute rank position in every other run
+// (a full binary search); entries then only search between their tile's splitters.
+__global__ void merge_split_kernel(MergeParams p) {
+  const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t g = x / p.nruns, s = x % p.nruns;
+  if (*p.flags || g >= p.tile_base[p.nruns]) return;
+  uint32_t r = 0;  // run of tile g
+  while (p.tile_base[r + 1] <= g) r++;
+  const uint32_t i = p.run_first[r] + (g - p.tile_base[r]) * kMergeTile;
+  uint32_t li;
+  const uint8_t* ki = key_of(p, i, li);
+  p.spl[(uint64_t)g * p.nruns + s] =
+      s == r ? i : rank_in(p, s, r, ki, li, p.run_first[s], p.run_first[s + 1]);
 }
 
 __global__ void merge_rank_kernel(MergeParams p) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.n || *p.flags) return;
   const uint32_t r = run_of(p, i);
+  const uint32_t j = i - p.run_first[r];
+  const uint32_t g = p.tile_base[r] + j / kMergeTile;
+  const bool last_tile = g + 1 == p.tile_base[r + 1];
   uint32_t li;
   const uint8_t* ki = key_of(p, i, li);
-  uint32_t pos = i - p.run_first[r];
+  uint32_t pos = j;
   for (uint32_t s = 0; s < p.nruns; s++) {
     if (s == r) continue;
-    // entries of run s that precede entry i: key < x, or key == x with s < r (lower nice)
-    uint32_t lo = p.run_first[s], hi = p.run_first[s + 1];
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      uint32_t lm;
-      const uint8_t* km = key_of(p, mid, lm);
-      const int c = cmp_keys(km, lm, ki, li);
-      if (c < 0 || (c == 0 && s < r)) lo = mid + 1; else hi = mid;
-    }
-    pos += lo - p.run_first[s];
+    const uint32_t lo = p.spl[(uint64_t)g * p.nruns + s];
+    const uint32_t hi = last_tile ? p.run_first[s + 1] : p.spl[(uint64_t)(g + 1) * p.nruns + s];
+    pos += rank_in(p, s, r, ki, li, lo, hi) - p.run_first[s];
   }
   p.dst[pos] = i;
 }
@@ -119,11 +149,7 @@ __global__ void merge_keep_kernel(MergeParams p) {
     if (q > 0) {  // bytes.Equal(key, curKey): the merged predecessor is the last candidate
       uint32_t lp;
       const uint8_t* kp = key_of(p, p.dst[q - 1], lp);
-      if (lp == li) {
-        uint32_t k = 0;
-        while (k < li && kp[k] == ki[k]) k++;
-        keep = k < li;
-      }
+      if (lp == li) keep = bytes_compare(kp, lp, ki, li) != 0;
     }
     if (keep) t = MTri{1, li, (uint64_t)(p.ve[i] - (i ? p.ve[i - 1] : 0u))};
   }
@@ -182,6 +208,12 @@ hipError_t launch_merge(const MergeParams& p, void* scan_tmp, size_t scan_bytes,
   if (p.n) {
     const dim3 g((p.n + 255) / 256), g8((uint32_t)(((uint64_t)p.n * 8 + 255) / 256));
     hipLaunchKernelGGL(merge_check_kernel, g, dim3(256), 0, s, p);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(merge_tiles_kernel, dim3(1), dim3(64), 0, s, p);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const uint64_t tiles = p.n / kMergeTile + p.nruns;  // >= the tile count
+    hipLaunchKernelGGL(merge_split_kernel, dim3((uint32_t)((tiles * p.nruns + 255) / 256)),
+                       dim3(256), 0, s, p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(merge_rank_kernel, g, dim3(256), 0, s, p);
     if ((e = hipGetLastError()) != hipSuccess) return e;

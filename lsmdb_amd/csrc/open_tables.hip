@@ -34,19 +34,6 @@ __device__ __forceinline__ uint32_t ld_be32(const uint8_t* p) {
   return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
 }
 
-// bytes.Compare
-__device__ int bytes_cmp(const uint8_t* a, uint32_t la, const uint8_t* b, uint32_t lb) {
-  const uint32_t n = la < lb ? la : lb;
-  for (uint32_t i = 0; i < n; i++)
-    if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
-  return la == lb ? 0 : (la < lb ? -1 : 1);
-}
-// y.CompareKeys (y.go:84-90): user key, then the 8-B timestamp suffix; both lengths > 8
-__device__ int compare_keys(const uint8_t* a, uint32_t la, const uint8_t* b, uint32_t lb) {
-  const int c = bytes_cmp(a, la - 8, b, lb - 8);
-  return c ? c : bytes_cmp(a + la - 8, 8, b + lb - 8, 8);
-}
-
 // table of block i: largest t with blk_base[t] <= i
 __device__ __forceinline__ uint32_t table_of(const uint32_t* base, uint32_t ntables, uint32_t i) {
   uint32_t lo = 0, hi = ntables - 1;
