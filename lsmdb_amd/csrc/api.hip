@@ -58,12 +58,8 @@ struct lsmgpu_ctx {
   DevBuf flags;          // encode flags
   DevBuf scan_tmp;
   DevBuf wsc;            // walk-scan-copy decode scratch (metadata, per-block triples)
-  DevBuf wsc_tmp;        // its scan temporary storage
   DevBuf open_tmp;       // batched table open: per-table scratch + scan temporary storage
   DevBuf merge_tmp;      // k-way merge: permutation, triples, scan, flags, scan storage
-  DevBuf wsc_carry;      // chunk carries ((kWscMaxChunks + 1) x 3 u64, [0..2] = 0)
-  hipStream_t aux = nullptr;               // walk-scan-copy: the copy kernels' stream
-  hipEvent_t wev[kWscMaxChunks + 1] = {};  // chunk c walked + scanned; [chunks] copies done
   // staging for host-memory calls
   DevBuf s_data, s_off, s_len, s_kd, s_ke, s_vd, s_ve, s_view, s_bf, s_bs, s_a, s_b, s_c, s_d;
 };
@@ -111,21 +107,6 @@ int lsmgpu_open(int device, lsmgpu_ctx** out) {
     return LSMGPU_ERR_HIP;
   }
   c->stream = c->own_stream;
-  if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) {
-    lsmgpu_close(c);
-    return LSMGPU_ERR_HIP;
-  }
-  for (hipEvent_t& ev : c->wev) {
-    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
-      lsmgpu_close(c);
-      return LSMGPU_ERR_HIP;
-    }
-  }
-  if (c->wsc_carry.ensure((kWscMaxChunks + 1) * 24) != hipSuccess ||
-      hipMemset(c->wsc_carry.p, 0, (kWscMaxChunks + 1) * 24) != hipSuccess) {
-    lsmgpu_close(c);
-    return LSMGPU_ERR_HIP;
-  }
   if (c->result.ensure(64) != hipSuccess || c->flags.ensure(64) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&c->h_result), 64, hipHostMallocDefault) != hipSuccess) {
     lsmgpu_close(c);
@@ -139,16 +120,12 @@ void lsmgpu_close(lsmgpu_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
-  if (c->aux) (void)hipStreamSynchronize(c->aux);
-  DevBuf* bufs[] = {&c->lb, &c->result, &c->flags, &c->scan_tmp, &c->wsc, &c->wsc_tmp,
-                    &c->wsc_carry, &c->open_tmp, &c->merge_tmp, &c->s_data,
+  DevBuf* bufs[] = {&c->lb, &c->result, &c->flags, &c->scan_tmp, &c->wsc,
+                    &c->open_tmp, &c->merge_tmp, &c->s_data,
                     &c->s_off, &c->s_len, &c->s_kd, &c->s_ke, &c->s_vd, &c->s_ve, &c->s_view,
                     &c->s_bf, &c->s_bs, &c->s_a, &c->s_b, &c->s_c, &c->s_d};
   for (DevBuf* b : bufs) b->release();
   if (c->h_result) (void)hipHostFree(c->h_result);
-  for (hipEvent_t ev : c->wev)
-    if (ev) (void)hipEventDestroy(ev);
-  if (c->aux) (void)hipStreamDestroy(c->aux);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }
@@ -266,11 +243,9 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     const size_t meta_b = (size_t)nblk * cap * 8;
     const size_t tri_b = ((size_t)nblk * 24 + 255) / 256 * 256;
     const size_t wneed = meta_b + 2 * tri_b + (size_t)nblk * 4;
-    const size_t sbytes = wsc_scan_bytes((uint32_t)nblk);
-    if (wneed > c->wsc.cap || sbytes > c->wsc_tmp.cap) {
+    if (wneed > c->wsc.cap) {
       HIPC(hipStreamSynchronize(c->stream));
       HIPC(c->wsc.ensure(wneed));
-      HIPC(c->wsc_tmp.ensure(sbytes));
     }
     uint8_t* w = c->wsc.as<uint8_t>();
     p.wmeta = reinterpret_cast<uint32_t*>(w);
@@ -281,12 +256,6 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     static const uint32_t ablate =
         getenv("LSMGPU_ABLATE") ? (uint32_t)atoi(getenv("LSMGPU_ABLATE")) : 0u;
     p.ablate = ablate;
-    // chunks overlap one chunk's copy with the next chunk's walk (LSMGPU_WSC_CHUNKS)
-    const char* ch_env = getenv("LSMGPU_WSC_CHUNKS");
-    const int chunks = ch_env ? atoi(ch_env) : kWscChunks;
-    const int nch = nblk >= (uint64_t)chunks * kWscMinBlocks ? chunks : 1;
-    p.wb0 = 0;
-    p.wb1 = (uint32_t)nblk;
     // big blocks: several waves copy one block (more bytes in flight per block); LSMGPU_WSC_SPLIT
     const char* sp_env = getenv("LSMGPU_WSC_SPLIT");
     uint32_t split = max_blk_len > 8192 ? 2u : 1u;  // measured: C5 1.25 -> 1.09 ms at 2
@@ -295,10 +264,7 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     const char* j_env = getenv("LSMGPU_WSC_J");  // A/B: lanes per entry in the copy
     p.wj = j_env ? (uint32_t)atoi(j_env) : 0u;
     if (p.wj != 8 && p.wj != 16) p.wj = 0;
-    const bool one_stream = getenv("LSMGPU_WSC_ONE_STREAM") != nullptr;
-    HIPC(launch_decode_wsc(p, c->wsc_tmp.p, c->wsc_tmp.cap, c->stream,
-                           one_stream ? nullptr : c->aux, c->wev,
-                           c->wsc_carry.as<uint64_t>(), nch));
+    HIPC(launch_decode_wsc(p, c->stream));
     return LSMGPU_OK;
   }
   uint64_t waves = 0;

@@ -1,25 +1,22 @@
-// decode_wsc.hip -- "walk, scan, copy" SST block decode for LARGE or irregular blocks
-// (BASELINE C5: Zipf 16-264 B keys in 32 KiB blocks; 100-entry blocks of C1/C4).
+// decode_wsc.hip -- "walk, scan, copy" SST block decode: the default path for batches of
+// >= 1,024 blocks < 64 KiB (BASELINE C2-C5), plus the fused tile kernel (a forced path).
 //
-// The speculative in-LDS walk of decode.hip confirms a whole run of equal-size entries per
-// round; with Zipf key lengths every entry has its own size, so it degenerates to one entry
-// per round and one 32 KiB block per wave (LDS).  Here the serial header chain is walked by
-// ONE LANE PER BLOCK straight from global memory -- 64 blocks per wave, thousands of blocks in
-// flight, each hop one dependent 8-B load -- and the bytes are then moved by a separate,
-// fully parallel copy with known output bases:
+// The serial header chain is walked by ONE LANE PER BLOCK straight from global memory -- 64
+// blocks per wave, every block of the batch in flight, each hop one dependent 8-B load -- and
+// the bytes are then moved by a separate, fully parallel copy with known output bases:
 //   K1 walk_kernel : lane b walks block b exactly like blockIterator.Next/parseKV
 //                    (table/iterator.go:93-135), writing per entry {pos | value offset << 16,
 //                    key offset} (full-line chunks, see flush_meta) and {entries, key
-//                    bytes, value bytes} + status per block
-//   scan           : rocPRIM exclusive scan of the per-block triples (device-wide)
-//   K2 copy_kernel : one wave per block; lane groups copy each entry's key and value as
-//                    unaligned 16-B pieces (the last overlapping back inside the entry, so
-//                    no store leaves it) global -> global, plus end offsets / view records
+//                    bytes, value bytes} + status per block; each 256-block workgroup then
+//                    scans its blocks and finds its base by decoupled look-back, so K1 ends
+//                    with every block's output base
+//   K2 copy_kernel : one wave per block (two above 8 KiB); lane groups copy each entry's key
+//                    and value as unaligned 16-B pieces (the last overlapping back inside the
+//                    entry, so no store leaves it) global -> global, plus end offsets / view
 // Traffic: the input is read twice (walk touches every line; copy reads the bytes) -- the
-// price of taking the serial walk off the critical path.  Blocks must be < 64 KiB.
+// price of taking the serial walk off the critical path (DESIGN.md).  Blocks must be < 64 KiB.
 #include <cstdlib>
 
-#include <rocprim/device/device_scan.hpp>
 
 #include "codec_common.hpp"
 #include "decode_common.hpp"
@@ -65,44 +62,105 @@ __device__ __forceinline__ void flush_meta(uint2* dst, const uint2* row, uint32_
   }
 }
 
-// K1: lane = block.
+// K1: lane = block; a workgroup = a tile of 256 consecutive blocks, tiles taken in ticket order
+// (p.gcnt[0]).  After the walk the workgroup scans its blocks' {entries, key bytes, value
+// bytes}, publishes the tile aggregate and finds the tile's output base by decoupled look-back
+// over the tile records (epoch-tagged granules in p.lb), then writes every block's exclusive
+// base: the output bases are known when the walk ends, with no separate scan launch.  The
+// ticket makes every predecessor tile already running, so the look-back always progresses.
 __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   __shared__ uint2 stage[256 * kWalkStage];
-  uint2* row = stage + threadIdx.x * kWalkStage;
-  const uint32_t b = p.wb0 + blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= p.wb1) return;
-  const uint32_t off = p.blk_off[b], len = p.blk_len[b];
-  uint32_t n = 0, K = 0, V = 0, st = LSMGPU_BLK_OK, pos = 0;
-  uint2* meta = reinterpret_cast<uint2*>(p.wmeta) + (uint64_t)b * p.wcap;
-  if ((uint64_t)off + len > p.data_len) {
-    st = LSMGPU_BLK_RANGE;
-  } else {
-    const uint8_t* blk = p.data + off;
-    for (;;) {
-      if (pos >= len) break;                                   // iterator.go:115-118
-      if (len - pos < 10) { st = LSMGPU_BLK_TRUNC_HEADER; break; }
-      uint32_t plen, klen, vlen;
-      read_hdr(blk + pos, plen, klen, vlen);                   // iterator.go:121
-      if ((klen | plen) == 0) break;                           // iterator.go:124-127
-      if (n == 0 && plen != 0) { st = LSMGPU_BLK_FIRST_PLEN; break; }  // iterator.go:129-133
-      if (10 + plen > len) { st = LSMGPU_BLK_PREFIX_OOB; break; }      // base key = entry 0's
-      const uint32_t end = pos + 10 + klen + vlen;             // iterator.go:101-109
-      if (end > len) { st = LSMGPU_BLK_VALUE_OVERFLOW; break; }
-      row[n & 15] = make_uint2(pos | (V << 16), K);  // n < wcap - 1: >= 10 B per entry
-      if ((n & 15) == 15) flush_meta(meta + (n - 15), row, 16);
-      K += plen + klen;
-      V += vlen;
-      n++;
-      pos = end;
+  __shared__ uint32_t s_tile;
+  __shared__ uint32_t s_wave[4][3];
+  __shared__ uint32_t s_ex[3];
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint32_t ntiles = (p.nblk + 255) / 256;
+  if (tid == 0) {
+    const uint32_t t = atomicAdd(p.gcnt, 1u);
+    if (t == ntiles - 1) atomicExch(p.gcnt, 0u);  // every ticket is taken
+    s_tile = t;
+  }
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  const uint32_t b = tile * 256 + tid;
+  uint32_t n = 0, K = 0, V = 0;
+  if (b < p.nblk) {
+    uint2* row = stage + tid * kWalkStage;
+    const uint32_t off = p.blk_off[b], len = p.blk_len[b];
+    uint32_t st = LSMGPU_BLK_OK, pos = 0;
+    uint2* meta = reinterpret_cast<uint2*>(p.wmeta) + (uint64_t)b * p.wcap;
+    if ((uint64_t)off + len > p.data_len) {
+      st = LSMGPU_BLK_RANGE;
+    } else {
+      const uint8_t* blk = p.data + off;
+      for (;;) {
+        if (pos >= len) break;                                   // iterator.go:115-118
+        if (len - pos < 10) { st = LSMGPU_BLK_TRUNC_HEADER; break; }
+        uint32_t plen, klen, vlen;
+        read_hdr(blk + pos, plen, klen, vlen);                   // iterator.go:121
+        if ((klen | plen) == 0) break;                           // iterator.go:124-127
+        if (n == 0 && plen != 0) { st = LSMGPU_BLK_FIRST_PLEN; break; }  // iterator.go:129-133
+        if (10 + plen > len) { st = LSMGPU_BLK_PREFIX_OOB; break; }      // base key = entry 0's
+        const uint32_t end = pos + 10 + klen + vlen;             // iterator.go:101-109
+        if (end > len) { st = LSMGPU_BLK_VALUE_OVERFLOW; break; }
+        row[n & 15] = make_uint2(pos | (V << 16), K);  // n < wcap - 1: >= 10 B per entry
+        if ((n & 15) == 15) flush_meta(meta + (n - 15), row, 16);
+        K += plen + klen;
+        V += vlen;
+        n++;
+        pos = end;
+      }
+    }
+    row[n & 15] = make_uint2(pos | (V << 16), K);
+    flush_meta(meta + (n & ~15u), row, (n & 15) + 1);
+    uint64_t* t = p.wstat + 3ull * b;
+    t[0] = n;
+    t[1] = K;
+    t[2] = V;
+    p.wstatus[b] = st;
+  }
+  // tile scan (saturating u32: a key stream past 4 GiB - 1 fails the copy's capacity check)
+  const uint32_t in_ = wave_scan_sat(n, lane), ik = wave_scan_sat(K, lane),
+                 iv = wave_scan_sat(V, lane);
+  if (lane == 63) {
+    s_wave[wave][0] = in_;
+    s_wave[wave][1] = ik;
+    s_wave[wave][2] = iv;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    uint32_t tn = 0, tk = 0, tv = 0;
+    for (int w = 0; w < 4; w++) {
+      tn = sat_add(tn, s_wave[w][0]);
+      tk = sat_add(tk, s_wave[w][1]);
+      tv = sat_add(tv, s_wave[w][2]);
+    }
+    uint64_t* R = p.lb + (uint64_t)tile * 8;
+    Tot ex{0, 0, 0};
+    if (tile > 0) {
+      store3(R, p.tag, tn, tk, tv, lane);
+      ex = lookback(p.lb, tile, p.tag, lane, p.result);
+    }
+    store3(R + 4, p.tag, sat_add(ex.n, tn), sat_add(ex.k, tk), sat_add(ex.v, tv), lane);
+    if (lane == 0) {
+      s_ex[0] = ex.n;
+      s_ex[1] = ex.k;
+      s_ex[2] = ex.v;
     }
   }
-  row[n & 15] = make_uint2(pos | (V << 16), K);
-  flush_meta(meta + (n & ~15u), row, (n & 15) + 1);
-  uint64_t* t = p.wstat + 3ull * b;
-  t[0] = n;
-  t[1] = K;
-  t[2] = V;
-  p.wstatus[b] = st;
+  __syncthreads();
+  if (b < p.nblk) {
+    uint32_t on = s_ex[0], ok = s_ex[1], ov = s_ex[2];
+    for (uint32_t w = 0; w < wave; w++) {
+      on = sat_add(on, s_wave[w][0]);
+      ok = sat_add(ok, s_wave[w][1]);
+      ov = sat_add(ov, s_wave[w][2]);
+    }
+    uint64_t* bs = p.wbase + 3ull * b;
+    bs[0] = sat_add(on, in_ - n);
+    bs[1] = sat_add(ok, ik == 0xffffffffu ? ik : ik - K);
+    bs[2] = sat_add(ov, iv - V);
+  }
 }
 
 // The entries of one block: J lanes per entry; an entry's pieces are [key pieces | value
@@ -183,8 +241,8 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   // p.wsplit waves share a block (large blocks): wave `sub` takes passes sub, sub + wsplit, ...
   const uint32_t wave = threadIdx.x >> 6, split = p.wsplit;
   const uint32_t sub = wave % split;
-  const uint32_t b = uniform(p.wb0 + blockIdx.x * (4 / split) + wave / split);
-  if (b >= p.wb1) return;
+  const uint32_t b = uniform(blockIdx.x * (4 / split) + wave / split);
+  if (b >= p.nblk) return;
   const uint64_t* t = p.wstat + 3ull * b;
   const uint32_t n = uniform((uint32_t)t[0]), K = uniform((uint32_t)t[1]),
                  V = uniform((uint32_t)t[2]);
@@ -527,71 +585,14 @@ hipError_t launch_decode_tile(const DecodeParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-namespace {
-struct Tri64 {
-  uint64_t n, k, v;
-};
-struct Tri64Plus {
-  __device__ __host__ Tri64 operator()(const Tri64& a, const Tri64& b) const {
-    return Tri64{a.n + b.n, a.k + b.k, a.v + b.v};
-  }
-};
-}  // namespace
-
-// chunk c's scan starts from carry[c] = the inclusive totals of every earlier chunk
-__global__ void wsc_carry_kernel(const uint64_t* wstat, const uint64_t* wbase, uint32_t last,
-                                 uint64_t* carry) {
-  if (threadIdx.x < 3) carry[threadIdx.x] = wbase[3ull * last + threadIdx.x] + wstat[3ull * last + threadIdx.x];
-}
-
-size_t wsc_scan_bytes(uint32_t nblk) {
-  size_t bytes = 0;
-  (void)rocprim::exclusive_scan(nullptr, bytes, (const Tri64*)nullptr, (Tri64*)nullptr,
-                                rocprim::future_value<Tri64>(nullptr), (size_t)nblk, Tri64Plus());
-  return bytes;
-}
-
-hipError_t launch_decode_wsc(const DecodeParams& p, void* scan_tmp, size_t scan_bytes,
-                             hipStream_t s, hipStream_t aux, hipEvent_t* ev, uint64_t* carry,
-                             int chunks) {
+hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s) {
   const uint32_t nblk = p.nblk;
-  if (chunks < 1) chunks = 1;
-  if (chunks > kWscMaxChunks) chunks = kWscMaxChunks;
-  if ((uint32_t)chunks > nblk) chunks = (int)nblk;
-  hipError_t e = hipSuccess;
-  for (int c = 0; c < chunks; c++) {
-    DecodeParams q = p;
-    q.wb0 = (uint32_t)((uint64_t)nblk * c / chunks);
-    q.wb1 = (uint32_t)((uint64_t)nblk * (c + 1) / chunks);
-    const uint32_t nb = q.wb1 - q.wb0;
-    hipLaunchKernelGGL(wsc_walk_kernel, dim3((nb + 255) / 256), dim3(256), 0, s, q);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    size_t bytes = scan_bytes;
-    e = rocprim::exclusive_scan(scan_tmp, bytes, reinterpret_cast<const Tri64*>(p.wstat + 3ull * q.wb0),
-                                reinterpret_cast<Tri64*>(p.wbase + 3ull * q.wb0),
-                                rocprim::future_value<Tri64>(reinterpret_cast<Tri64*>(carry + 3 * c)),
-                                (size_t)nb, Tri64Plus(), s);
-    if (e != hipSuccess) return e;
-    if (c + 1 < chunks) {
-      hipLaunchKernelGGL(wsc_carry_kernel, dim3(1), dim3(64), 0, s, p.wstat, p.wbase, q.wb1 - 1,
-                         carry + 3 * (c + 1));
-      if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
-    hipStream_t cs = s;
-    if (chunks > 1 && aux) {
-      if ((e = hipEventRecord(ev[c], s)) != hipSuccess) return e;
-      if ((e = hipStreamWaitEvent(aux, ev[c], 0)) != hipSuccess) return e;
-      cs = aux;
-    }
-    const uint32_t per_wg = 4 / q.wsplit;  // blocks per 4-wave workgroup
-    hipLaunchKernelGGL(wsc_copy_kernel, dim3((nb + per_wg - 1) / per_wg), dim3(256), 0, cs, q);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-  }
-  if (chunks > 1 && aux) {
-    if ((e = hipEventRecord(ev[chunks], aux)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(s, ev[chunks], 0)) != hipSuccess) return e;
-  }
-  return hipSuccess;
+  hipLaunchKernelGGL(wsc_walk_kernel, dim3((nblk + 255) / 256), dim3(256), 0, s, p);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const uint32_t per_wg = 4 / p.wsplit;  // blocks per 4-wave workgroup
+  hipLaunchKernelGGL(wsc_copy_kernel, dim3((nblk + per_wg - 1) / per_wg), dim3(256), 0, s, p);
+  return hipGetLastError();
 }
 
 }  // namespace lsmgpu

@@ -29,7 +29,7 @@ struct DecodeParams {
   int32_t* blk_status;
   uint64_t* lb;             // per-block records: aggregate [0..2], exclusive prefix [4..6]
   uint64_t* glb;            // per-group records (64 blocks): aggregate [0..2], inclusive [4..6]
-  uint32_t* gcnt;           // [0]: the fused tile kernel's ticket (0 between launches)
+  uint32_t* gcnt;           // [0]: tile ticket of the walk / fused tile kernels (0 between launches)
   uint64_t* result;         // 8 u64, zeroed before launch
   uint32_t tag;             // 24-bit epoch tag of this launch
   uint32_t ablate;          // timing-only diagnostics (LSMGPU_ABLATE): 1 no prefix, 2 no emit, 4 no walk
@@ -42,7 +42,6 @@ struct DecodeParams {
   uint64_t* wstat;
   uint64_t* wbase;
   uint32_t* wstatus;
-  uint32_t wb0, wb1;        // walk-scan-copy: this launch's block range [wb0, wb1)
   uint32_t wsplit;          // walk-scan-copy: waves per block in the copy (1, 2 or 4)
   uint32_t wj;              // walk-scan-copy: lanes per entry forced (8, 16), 0 = per block
 };
@@ -124,17 +123,9 @@ hipError_t launch_merge(const MergeParams& p, void* scan_tmp, size_t scan_bytes,
 hipError_t launch_decode(const DecodeParams& p, uint32_t max_blk_len, int num_cus,
                          hipStream_t s, uint64_t* waves_launched);
 hipError_t launch_encode(const EncodeParams& p, int num_cus, hipStream_t s);
-// walk-scan-copy decode (blocks of 4 KiB .. 64 KiB - 1): scratch sized by the caller
-size_t wsc_scan_bytes(uint32_t nblk);
-// Chunked over `chunks` block ranges: walk + scan (+ carry) of chunk c on `s`, its copy on
-// `aux` after an event, so chunk c's copy overlaps chunk c+1's walk; `s` finally waits for
-// `aux`.  aux == nullptr: every chunk's copy on `s` right after its walk (the copy re-reads
-// lines the walk just pulled through the 256 MiB Infinity Cache).  `ev` holds chunks + 1 events, `carry` (chunks + 1) x 3 u64 with carry[0..2] = 0.
-constexpr int kWscMaxChunks = 16;
-constexpr int kWscChunks = 1;  // default chunk count (measured: DESIGN.md)
-hipError_t launch_decode_wsc(const DecodeParams& p, void* scan_tmp, size_t scan_bytes,
-                             hipStream_t s, hipStream_t aux, hipEvent_t* ev, uint64_t* carry,
-                             int chunks);
+// walk-scan-copy decode (blocks < 64 KiB): scratch (wmeta, wstat, wbase, wstatus) sized by
+// the caller; p.gcnt[0] = 0 between launches (the walk's tile ticket), p.lb tile records
+hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s);
 // fused tile decode (blocks <= 4 KiB): one launch, ticket-ordered tiles (p.gcnt[0] = 0)
 hipError_t launch_decode_tile(const DecodeParams& p, hipStream_t s);
 // which decode path a batch takes: 0 register-lag (<= 4 KiB), 1 LDS-lag, 2 walk-scan-copy

@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out/wscj
 for J in 16 8; do
-LSMGPU_WSC_J=$J timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "split or forced or large or chunked" > gpurun_out/wscj/tests$J.log 2>&1 || { tail -30 gpurun_out/wscj/tests$J.log; exit 1; }
+LSMGPU_WSC_J=$J timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "split or forced or large or tiles" > gpurun_out/wscj/tests$J.log 2>&1 || { tail -30 gpurun_out/wscj/tests$J.log; exit 1; }
 tail -1 gpurun_out/wscj/tests$J.log
 done
 for cfg in 5 2 4; do for J in auto 8 16; do

@@ -315,24 +315,6 @@ def test_forced_decode_paths(codec, oracle, monkeypatch, path):
     test_prefix_compressed_random(codec, oracle)
 
 
-@pytest.mark.parametrize("chunks", [2, 3, 8])
-def test_wsc_chunked(codec, oracle, monkeypatch, chunks):
-    """Walk-scan-copy split into block-range chunks: chunk c's copy runs on the auxiliary stream
-    while chunk c+1 is walked; each chunk's scan starts from the device-side carry of the
-    chunks before it.  Ragged chunk boundaries (nblk not a multiple of the chunk count)."""
-    monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
-    monkeypatch.setenv("LSMGPU_WSC_CHUNKS", str(chunks))
-    c = _cols(2, 34 * 1024 * chunks + 777, seed=21)
-    sst, _, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, 0, 4096)
-    sst = sst + b"{}" + (2).to_bytes(4, "big")
-    off, ln, _, _ = oracle.parse_index(sst)
-    assert len(off) >= 1024 * chunks
-    g = codec.decode_host(sst, off, ln)
-    _assert_same(g, oracle.decode(sst, off, ln), f"chunks={chunks}")
-    assert g.key_data.tobytes() == c.keys.tobytes()
-    assert g.val_data.tobytes() == c.vs.tobytes()
-
-
 @pytest.mark.parametrize("split", [1, 2, 4])
 def test_wsc_split(codec, oracle, monkeypatch, split):
     """Walk-scan-copy with 1, 2 or 4 waves sharing each block's copy (LSMGPU_WSC_SPLIT): C5
@@ -390,3 +372,18 @@ def test_prefix_compressed_large_output(codec, oracle, monkeypatch, path):
     ref = oracle.decode(data, off, ln)
     assert int(ref.key_end[int(ref.blk_first[1]) - 1]) > 65536  # the first block's keys alone
     _assert_same(codec.decode_host(data, off, ln), ref, f"path={path}")
+
+
+def test_wsc_many_tiles(codec, oracle):
+    """The walk kernel's tiles (256 blocks, ticket order) find their output bases by decoupled
+    look-back over ~40 tile records: C2 blocks plus a ragged last tile, checked against the
+    oracle on every output array."""
+    c = _cols(2, 330000, seed=13)
+    sst, _, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, 0, 4096)
+    sst = sst + b"{}" + (2).to_bytes(4, "big")
+    off, ln, _, _ = oracle.parse_index(sst)
+    assert len(off) > 39 * 256 and len(off) % 256 != 0
+    g = codec.decode_host(sst, off, ln)
+    _assert_same(g, oracle.decode(sst, off, ln), "many tiles")
+    assert g.key_data.tobytes() == c.keys.tobytes()
+    assert g.val_data.tobytes() == c.vs.tobytes()
