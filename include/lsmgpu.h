@@ -227,6 +227,31 @@ typedef struct {
 int lsmgpu_merge_runs_async(lsmgpu_ctx* ctx, const lsmgpu_runs* in, const lsmgpu_merged* out,
                             uint64_t* d_result);
 
+/* ---- Compaction output tables (levels.go:259-271 with Builder.ReachedCapacity) ------------
+ * Cut a sorted entry stream (e.g. the merge output) into tables exactly where compactBuildTables
+ * starts a new Builder: before each Add, ReachedCapacity(cap) = buf.Len() + 8 + 4*len(restarts)
+ * + 8 > cap (table/builder.go:140-143) with entries_per_block entries per block (100 =
+ * resultInterval).  Outputs (device): tbl_first[t] = first entry of table t, tbl_blk[t] = first
+ * block, tbl_out[t] = byte offset of its image; entry [ntables] closes each array.  Images are
+ * "Finish minus bloom" ([blocks][restarts BE32 x N][N BE32], like lsmgpu_encode_blocks), back
+ * to back.  d_result (8 u64): [0] tables, [1] blocks, [2] image bytes, [3] 1 if tables_cap
+ * was too small. */
+int lsmgpu_cut_tables_async(lsmgpu_ctx* ctx, const uint32_t* d_key_end, const uint32_t* d_vs_end,
+                            uint64_t n, uint32_t entries_per_block, int64_t cap,
+                            uint32_t* d_tbl_first, uint32_t* d_tbl_blk, uint64_t* d_tbl_out,
+                            uint32_t tables_cap, uint64_t* d_result);
+/* Encodes every table of a cut (one launch over all their blocks) into d_out (sized for the
+ * cut's image bytes).  max_blocks bounds the tables' total block count (grid size), e.g.
+ * ceil(n / entries_per_block) + tables_cap.  key_total / vs_total (0 if unknown) pick the lanes
+ * per entry.  d_flags as lsmgpu_encode_blocks_async. */
+int lsmgpu_encode_tables_async(lsmgpu_ctx* ctx, const uint8_t* d_keys, const uint32_t* d_key_end,
+                               const uint8_t* d_vs, const uint32_t* d_vs_end, uint64_t n,
+                               uint64_t key_total, uint64_t vs_total,
+                               uint32_t entries_per_block, const uint32_t* d_tbl_first,
+                               const uint32_t* d_tbl_blk, const uint64_t* d_tbl_out,
+                               uint32_t tables_cap, uint64_t max_blocks, uint8_t* d_out,
+                               uint32_t* d_flags);
+
 #ifdef __cplusplus
 }
 #endif

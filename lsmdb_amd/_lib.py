@@ -49,6 +49,8 @@ EXPORTED_SYMBOLS = (
     "lsmgpu_parse_index",
     "lsmgpu_open_tables_async",
     "lsmgpu_merge_runs_async",
+    "lsmgpu_cut_tables_async",
+    "lsmgpu_encode_tables_async",
     "lsmgpu_decode_blocks",
     "lsmgpu_decode_blocks_async",
     "lsmgpu_encode_blocks",
@@ -180,6 +182,15 @@ def _load() -> ctypes.CDLL:
     lib.lsmgpu_open_tables_async.restype = c_int
     lib.lsmgpu_merge_runs_async.argtypes = [c_void_p, POINTER(Runs), POINTER(Merged), c_void_p]
     lib.lsmgpu_merge_runs_async.restype = c_int
+    lib.lsmgpu_cut_tables_async.argtypes = [c_void_p, c_void_p, c_void_p, c_uint64, c_uint32,
+                                            ctypes.c_int64, c_void_p, c_void_p, c_void_p,
+                                            c_uint32, c_void_p]
+    lib.lsmgpu_cut_tables_async.restype = c_int
+    lib.lsmgpu_encode_tables_async.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                               c_uint64, c_uint64, c_uint64, c_uint32, c_void_p,
+                                               c_void_p, c_void_p, c_uint32, c_uint64, c_void_p,
+                                               c_void_p]
+    lib.lsmgpu_encode_tables_async.restype = c_int
     return lib
 
 

@@ -382,6 +382,54 @@ class Codec:
                 o["src"][:m].cpu().numpy().view(np.uint32), int(r[3]))
 
 
+    # -- compaction output tables (Builder.ReachedCapacity cut + one encode over every table)
+    def cut_tables_device(self, key_end, vs_end, n: int, cap: int, entries_per_block: int = 100,
+                          tables_cap: int = 4096) -> dict:
+        """lsmgpu_cut_tables_async (asynchronous): device tensors tbl_first / tbl_blk /
+        tbl_out / result."""
+        import torch
+        dev = key_end.device
+        o = dict(tbl_first=torch.empty(tables_cap + 1, dtype=torch.int32, device=dev),
+                 tbl_blk=torch.empty(tables_cap + 1, dtype=torch.int32, device=dev),
+                 tbl_out=torch.empty(tables_cap + 1, dtype=torch.int64, device=dev),
+                 result=torch.zeros(8, dtype=torch.int64, device=dev),
+                 tables_cap=tables_cap, epb=entries_per_block, n=n)
+        check(lib().lsmgpu_cut_tables_async(self._ctx, _ptr(key_end), _ptr(vs_end), n,
+                                            entries_per_block, cap, _ptr(o["tbl_first"]),
+                                            _ptr(o["tbl_blk"]), _ptr(o["tbl_out"]), tables_cap,
+                                            _ptr(o["result"])), "cut_tables_async")
+        return o
+
+    def encode_tables_device(self, cut: dict, keys, key_end, vs, vs_end, key_total: int,
+                             vs_total: int, out, flags) -> None:
+        """lsmgpu_encode_tables_async over a cut (asynchronous)."""
+        n, epb, tc = cut["n"], cut["epb"], cut["tables_cap"]
+        check(lib().lsmgpu_encode_tables_async(self._ctx, _ptr(keys), _ptr(key_end), _ptr(vs),
+                                               _ptr(vs_end), n, key_total, vs_total, epb,
+                                               _ptr(cut["tbl_first"]), _ptr(cut["tbl_blk"]),
+                                               _ptr(cut["tbl_out"]), tc, (n + epb - 1) // epb + tc,
+                                               _ptr(out), _ptr(flags)), "encode_tables_async")
+
+    def compact_tables_device(self, keys, key_end, vs, vs_end, n: int, key_total: int,
+                              vs_total: int, cap: int, entries_per_block: int = 100,
+                              tables_cap: int = 4096) -> dict:
+        """Cut the sorted stream into compactBuildTables' output tables and encode them all;
+        synchronizes once to size the output.  Returns device tensors: out (images back to
+        back), tbl_first / tbl_blk / tbl_out, result, flags."""
+        import torch
+        o = self.cut_tables_device(key_end, vs_end, n, cap, entries_per_block, tables_cap)
+        self.synchronize()
+        r = o["result"].cpu().numpy()
+        if r[3]:
+            raise LsmgpuError(_lib.ERR_CAPACITY, "cut_tables: more tables than tables_cap")
+        o["ntables"], o["bytes"] = int(r[0]), int(r[2])
+        o["out"] = torch.empty(max(o["bytes"], 16) + 16, dtype=torch.uint8, device=key_end.device)
+        o["flags"] = torch.zeros(4, dtype=torch.int32, device=key_end.device)
+        self.encode_tables_device(o, keys, key_end, vs, vs_end, key_total, vs_total, o["out"],
+                                  o["flags"])
+        return o
+
+
 _DEFAULT: dict[int, Codec] = {}
 
 

@@ -668,4 +668,63 @@ int lsmgpu_merge_runs_async(lsmgpu_ctx* c, const lsmgpu_runs* in, const lsmgpu_m
   return LSMGPU_OK;
 }
 
+// ------------------------------------------------------------------ compaction output tables
+int lsmgpu_cut_tables_async(lsmgpu_ctx* c, const uint32_t* d_key_end, const uint32_t* d_vs_end,
+                            uint64_t n, uint32_t entries_per_block, int64_t cap,
+                            uint32_t* d_tbl_first, uint32_t* d_tbl_blk, uint64_t* d_tbl_out,
+                            uint32_t tables_cap, uint64_t* d_result) {
+  if (!c || !d_tbl_first || !d_tbl_blk || !d_tbl_out || !d_result) return LSMGPU_ERR_ARG;
+  if (n && (!d_key_end || !d_vs_end)) return LSMGPU_ERR_ARG;
+  if (entries_per_block == 0 || tables_cap == 0) return LSMGPU_ERR_ARG;
+  if (n > 0xffffffffull) return LSMGPU_ERR_TOO_LARGE;
+  HIPC(hipSetDevice(c->device));
+  HIPC(hipMemsetAsync(d_result, 0, 8 * sizeof(uint64_t), c->stream));
+  CutParams p{};
+  p.key_end = d_key_end;
+  p.vs_end = d_vs_end;
+  p.n = n;
+  p.epb = entries_per_block;
+  p.cap = cap;
+  p.tbl_first = d_tbl_first;
+  p.tbl_blk = d_tbl_blk;
+  p.tbl_out = d_tbl_out;
+  p.tables_cap = tables_cap;
+  p.result = d_result;
+  HIPC(launch_cut_tables(p, c->stream));
+  return LSMGPU_OK;
+}
+
+int lsmgpu_encode_tables_async(lsmgpu_ctx* c, const uint8_t* d_keys, const uint32_t* d_key_end,
+                               const uint8_t* d_vs, const uint32_t* d_vs_end, uint64_t n,
+                               uint64_t key_total, uint64_t vs_total,
+                               uint32_t entries_per_block, const uint32_t* d_tbl_first,
+                               const uint32_t* d_tbl_blk, const uint64_t* d_tbl_out,
+                               uint32_t tables_cap, uint64_t max_blocks, uint8_t* d_out,
+                               uint32_t* d_flags) {
+  if (!c || !d_tbl_first || !d_tbl_blk || !d_tbl_out || !d_out || !d_flags) return LSMGPU_ERR_ARG;
+  if (n && (!d_keys || !d_key_end || !d_vs || !d_vs_end)) return LSMGPU_ERR_ARG;
+  if (entries_per_block == 0 || tables_cap == 0) return LSMGPU_ERR_ARG;
+  if (max_blocks > 0xffffffffull || n > 0xffffffffull) return LSMGPU_ERR_TOO_LARGE;
+  if (n == 0) return LSMGPU_OK;
+  HIPC(hipSetDevice(c->device));
+  EncodeParams p{};
+  p.keys = d_keys;
+  p.key_end = d_key_end;
+  p.vs = d_vs;
+  p.vs_end = d_vs_end;
+  p.n = n;
+  p.key_total = key_total;
+  p.vs_total = vs_total;
+  p.epb = entries_per_block;
+  p.nblocks = (uint32_t)max_blocks;
+  p.out = d_out;
+  p.flags = d_flags;
+  p.tbl_first = d_tbl_first;
+  p.tbl_blk = d_tbl_blk;
+  p.tbl_out = d_tbl_out;
+  p.ntables = tables_cap;  // the kernel reads the real count from the arrays' closing entries
+  HIPC(launch_encode(p, c->num_cus, c->stream));
+  return LSMGPU_OK;
+}
+
 }  // extern "C"

@@ -59,28 +59,60 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
                                            // trip, every offset load issued first
   const uint32_t lane = lane_id();
   const uint32_t b = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
-  if (b >= p.nblocks) return;
-  uint64_t f, l;
-  block_range(p, b, f, l);
+  // table context: output image, its data length, block count, and the entry / key / vs bases
+  // positions are relative to (one table, or table t of a compaction's output in tbl_* mode)
+  uint64_t f, l, e0b = 0, kb0 = 0, vb0 = 0, dl = p.data_len;
+  uint32_t lb = b, tnb = p.nblocks;
+  uint8_t* out = p.out;
+  if (p.tbl_first) {
+    if (b >= p.tbl_blk[p.ntables]) return;
+    uint32_t lo = 0, hi = p.ntables - 1;  // table of block b: largest t with tbl_blk[t] <= b
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (p.tbl_blk[mid] <= b) lo = mid; else hi = mid - 1;
+    }
+    const uint32_t t = uniform(lo);
+    lb = b - p.tbl_blk[t];
+    tnb = p.tbl_blk[t + 1] - p.tbl_blk[t];
+    e0b = p.tbl_first[t];
+    const uint64_t ee = p.tbl_first[t + 1];
+    f = e0b + (uint64_t)lb * p.epb;
+    l = f + p.epb < ee ? f + p.epb : ee;
+    kb0 = key_start(p, e0b);
+    vb0 = vs_start(p, e0b);
+    out = p.out + p.tbl_out[t];
+    dl = 10 * (ee - e0b) + (key_start(p, ee) - kb0) + (vs_start(p, ee) - vb0) + 13ull * tnb;
+  } else {
+    if (b >= p.nblocks) return;
+    block_range(p, b, f, l);
+  }
   f = uniform64(f);
   l = uniform64(l);
+  e0b = uniform64(e0b);
+  kb0 = uniform64(kb0);
+  vb0 = uniform64(vb0);
+  dl = uniform64(dl);
   const uint64_t m = l - f;
-  const uint32_t blk13 = 13u * b;
+  const uint32_t blk13 = 13u * lb;
+  // entry e's position in its table: 10 (e - e0b) + key bytes + vs bytes before it + 13 per block
+  auto position = [&](uint64_t e, uint64_t ks, uint64_t vs0) -> uint32_t {
+    return (uint32_t)(10 * (e - e0b) + (ks - kb0) + (vs0 - vb0)) + blk13;
+  };
 
   if (m == 0) {  // a block of no entries: the terminator alone (table_test.go:514)
     if (lane == 0) {
-      const uint32_t bs = (uint32_t)(10 * f + key_start(p, f) + vs_start(p, f)) + blk13;
-      uint8_t* t = p.out + bs;
+      const uint32_t bs = position(f, key_start(p, f), vs_start(p, f));
+      uint8_t* t = out + bs;
       store_header(t, 0, 3, 0xffffffffu);
       t[10] = 0;
       t[11] = 0;
       t[12] = 0;
-      store_be32(p.out + p.data_len + 4ull * b, bs + 13);
+      store_be32(out + dl + 4ull * lb, bs + 13);
     }
-    if (lane == 1 && b == p.nblocks - 1) store_be32(p.out + p.data_len + 4ull * p.nblocks, p.nblocks);
+    if (lane == 1 && lb == tnb - 1) store_be32(out + dl + 4ull * tnb, tnb);
     return;
   }
-  if (lane == 1 && b == p.nblocks - 1) store_be32(p.out + p.data_len + 4ull * p.nblocks, p.nblocks);
+  if (lane == 1 && lb == tnb - 1) store_be32(out + dl + 4ull * tnb, tnb);
 
   // Absolute entry positions are closed-form (no block base needed to place bytes); the block
   // start is entry f's position (lane 0, first pass), a header's prev is the previous entry's
@@ -102,7 +134,7 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
       const uint64_t kl64 = p.key_end[e] - ks[i], vl64 = p.vs_end[e] - vs0[i];
       klen[i] = (uint32_t)kl64;
       vlen[i] = (uint32_t)vl64;
-      pos[i] = (uint32_t)(10 * e + ks[i] + vs0[i]) + blk13;
+      pos[i] = position(e, ks[i], vs0[i]);
       if (on[i] && j == 0) {
         if (kl64 <= 8 || kl64 > 0xffff) bad |= 1;  // ParseKey needs len(key) > 8 (y.go:93-100)
         if (vl64 > 0xffff) bad |= 2;                // header vlen is a uint16
@@ -118,15 +150,15 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
       const uint32_t edge = i == 0 ? carry : readlane(pos[i - 1], kWave - J);
       const uint64_t r = e0 + i * EPP + lane / J;
       const uint32_t prev = r == 0 ? 0xffffffffu : (lane < J ? edge : below) - bs;  // builder.go:95-99
-      if (on[i] && j == 0) store_header(p.out + pos[i], klen[i], vlen[i], prev);
+      if (on[i] && j == 0) store_header(out + pos[i], klen[i], vlen[i], prev);
       if (on[i] && j == 1 && r == m - 1) {  // terminator + restart (builder.go:121-123,146-160)
         const uint32_t te = pos[i] + 10 + klen[i] + vlen[i];
-        uint8_t* t = p.out + te;
+        uint8_t* t = out + te;
         store_header(t, 0, 3, pos[i] - bs);
         t[10] = 0;
         t[11] = 0;
         t[12] = 0;
-        store_be32(p.out + p.data_len + 4ull * b, te + 13);
+        store_be32(out + dl + 4ull * lb, te + 13);
       }
     }
     carry = readlane(pos[G - 1], kWave - J);
@@ -134,7 +166,7 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
     for (uint32_t i = 0; i < G; i++) {
       for (uint32_t q = j; q < np[i]; q += J) {  // one (non-divergent) copy per piece
         const bool key = q < kp[i];
-        copy_piece16(p.out + pos[i] + 10 + (key ? 0u : klen[i]), key ? p.keys + ks[i] : p.vs + vs0[i],
+        copy_piece16(out + pos[i] + 10 + (key ? 0u : klen[i]), key ? p.keys + ks[i] : p.vs + vs0[i],
                   key ? klen[i] : vlen[i], key ? q : q - kp[i]);
       }
     }
@@ -142,8 +174,75 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
   if (bad) atomicOr(p.flags, bad);
 }
 
+// Builder.ReachedCapacity (builder.go:140-143) as compactBuildTables applies it before every
+// Add (levels.go:265-271): a table holding e entries [s, s + e) is closed when
+//   10e + K + V + 13 fb + 8 + 4 fb + 8 > cap,   fb = (e - 1) / epb finished blocks
+// (buf.Len() = every entry + each finished block's 13-B terminator; len(restarts) = fb), K, V
+// the key / vs bytes of those entries.  The predicate grows with e, so each cut is a search:
+// one wave, 64 candidate counts per round trip.  A table ends at the first e >= 1 where it
+// holds, or takes every remaining entry.  Image size = data + 4 (blocks) + 4 (block count).
+__global__ void cut_tables_kernel(CutParams p) {
+  const uint32_t lane = lane_id();
+  uint64_t s = 0, blocks = 0, bytes = 0;
+  uint32_t t = 0;
+  auto kstart = [&](uint64_t e) -> uint64_t { return e ? p.key_end[e - 1] : 0; };
+  auto vstart = [&](uint64_t e) -> uint64_t { return e ? p.vs_end[e - 1] : 0; };
+  while (s < p.n) {
+    if (t >= p.tables_cap) {
+      if (lane == 0) p.result[3] = 1;
+      break;
+    }
+    const uint64_t ks = kstart(s), vs = vstart(s), rest = p.n - s;
+    // first e in [1, rest - 1] with the predicate, or `rest` (all of them)
+    uint64_t lo = 1, hi = rest;
+    while (lo < hi) {
+      const uint64_t step = (hi - lo + 62) / 63;  // lane 63 reaches hi: the ballot is never empty
+      const uint64_t e = lo + lane * step < hi ? lo + lane * step : hi;
+      bool over = true;  // e == hi: the sentinel
+      if (e < hi) {
+        const uint64_t fb = (e - 1) / p.epb;
+        const int64_t est = (int64_t)(10 * e + (kstart(s + e) - ks) + (vstart(s + e) - vs) +
+                                      13 * fb + 8 + 4 * fb + 8);
+        over = est > p.cap;
+      }
+      const uint64_t mask = __ballot(over);
+      const uint32_t first = (uint32_t)__builtin_ctzll(mask);  // lane 63 or the clamp is true
+      const uint64_t ef = lo + (uint64_t)first * step < hi ? lo + (uint64_t)first * step : hi;
+      lo = first ? lo + (uint64_t)(first - 1) * step + 1 : lo;
+      hi = ef;
+    }
+    const uint64_t cnt = lo;
+    const uint64_t nb = (cnt + p.epb - 1) / p.epb;
+    if (lane == 0) {
+      p.tbl_first[t] = (uint32_t)s;
+      p.tbl_blk[t] = (uint32_t)blocks;
+      p.tbl_out[t] = bytes;
+    }
+    bytes += 10 * cnt + (kstart(s + cnt) - ks) + (vstart(s + cnt) - vs) + 13 * nb + 4 * nb + 4;
+    blocks += nb;
+    s += cnt;
+    t++;
+  }
+  for (uint32_t k = t + lane; k <= p.tables_cap; k += kWave) {  // close through tables_cap
+    p.tbl_first[k] = (uint32_t)s;
+    p.tbl_blk[k] = (uint32_t)blocks;
+    p.tbl_out[k] = bytes;
+  }
+  if (lane == 0) {
+    p.result[0] = t;
+    p.result[1] = blocks;
+    p.result[2] = bytes;
+  }
+}
+
+hipError_t launch_cut_tables(const CutParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(cut_tables_kernel, dim3(1), dim3(64), 0, s, p);
+  return hipGetLastError();
+}
+
 template <uint32_t J, uint32_t G>
 static hipError_t launch_enc(const EncodeParams& p, hipStream_t s) {
+  // tbl_* mode: p.nblocks is an upper bound on the blocks of all tables (grid size)
   hipLaunchKernelGGL((encode_kernel<J, G>), dim3((p.nblocks + 3) / 4), dim3(256), 0, s, p);
   return hipGetLastError();
 }
@@ -151,7 +250,7 @@ static hipError_t launch_enc(const EncodeParams& p, hipStream_t s) {
 hipError_t launch_encode(const EncodeParams& p, int num_cus, hipStream_t s) {
   (void)num_cus;
   // J = lanes per entry ~ the average entry's 16-B pieces (C2: 129 B -> 8; C3: ~1.1 KB -> 64)
-  const uint64_t avg = p.n ? (p.key_total + p.vs_total) / p.n : 0;
+  const uint64_t avg = p.n ? (p.key_total + p.vs_total) / p.n : 120;
   const char* ge = getenv("LSMGPU_ENC_G");  // A/B: entry-group passes per loop trip
   const int g = ge ? atoi(ge) : 1;           // measured: C2 G=1 0.61 ms, 2 0.68, 4 0.72
   const char* je = getenv("LSMGPU_ENC_J");   // A/B: lanes per entry

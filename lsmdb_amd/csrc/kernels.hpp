@@ -61,7 +61,28 @@ struct EncodeParams {
   uint8_t* out;
   uint64_t data_len;          // size of the data region (index starts here)
   uint32_t* flags;
+  // multi-table mode (tbl_first != nullptr): table t = entries [tbl_first[t], tbl_first[t+1]),
+  // blocks [tbl_blk[t], tbl_blk[t+1]) of epb entries, image at out + tbl_out[t]
+  const uint32_t* tbl_first;
+  const uint32_t* tbl_blk;
+  const uint64_t* tbl_out;
+  uint32_t ntables;
 };
+
+// Builder.ReachedCapacity table cut over a sorted entry stream (encode.hip)
+struct CutParams {
+  const uint32_t* key_end;
+  const uint32_t* vs_end;
+  uint64_t n;
+  uint32_t epb;
+  int64_t cap;
+  uint32_t* tbl_first;  // tables_cap + 1
+  uint32_t* tbl_blk;    // tables_cap + 1
+  uint64_t* tbl_out;    // tables_cap + 1
+  uint32_t tables_cap;
+  uint64_t* result;     // [0] tables, [1] blocks, [2] image bytes, [3] overflow
+};
+hipError_t launch_cut_tables(const CutParams& p, hipStream_t s);
 
 struct ValuesParams {
   const uint8_t* meta;

@@ -2,7 +2,10 @@
 table merged with the concatenated bottom tables), device-resident end to end:
   decode  all blocks of the 1 + 8 input tables (64 MiB each, C4 shape) in one batch
   merge   2 runs (top = nice 0, bottom = nice 1): y.MergeIterator, top wins on equal keys
-  encode  the merged stream as 100-entry blocks (Builder.Add / finishBlock)
+  cut     the merged stream into output tables where Builder.ReachedCapacity(64 MiB) starts a
+          new one (levels.go:265-271)
+  encode  every output table (100-entry blocks, Builder.Add / finishBlock / blockIndex) in one
+          launch
 Top keys are updates of every 8th bottom key (same key, new value): the merge drops 1/9 of its
 input.  HIP-event times (median of 5) per stage; the oracle merge (sstref_merge, 1 thread)
 timed on the host for the same runs; the merged keys/values checked against it.
@@ -102,14 +105,15 @@ def main():
     r = m["result"].cpu().numpy()
     n_out, kb, vb = int(r[0]), int(r[1]), int(r[2])
 
-    mk, mke = m["key_data"][:kb].contiguous(), m["key_end"][:n_out].contiguous()
-    mv, mve = m["val_data"][:vb].contiguous(), m["val_end"][:n_out].contiguous()
-    nb_out = (n_out + 99) // 100
-    out_len = 10 * n_out + kb + vb + 13 * nb_out + 4 * nb_out + 4
-    d_out = torch.empty(out_len + 16, dtype=torch.uint8, device=dev)
+    # output tables: ReachedCapacity(64 MiB) cut, then every table encoded in one launch
+    mk, mke, mv, mve = m["key_data"], m["key_end"], m["val_data"], m["val_end"]
+    t_cut, cut = timed(torch, stream, lambda: codec.cut_tables_device(mke, mve, n_out, 64 << 20))
+    cr = cut["result"].cpu().numpy()
+    ntab_out, out_bytes = int(cr[0]), int(cr[2])
+    d_out = torch.empty(out_bytes + 16, dtype=torch.uint8, device=dev)
     fl = torch.zeros(4, dtype=torch.int32, device=dev)
-    t_enc, _ = timed(torch, stream, lambda: codec.encode_device_async(
-        mk, mke, mv, mve, n_out, kb, vb, d_out, fl, entries_per_block=100))
+    t_enc, _ = timed(torch, stream, lambda: codec.encode_tables_device(
+        cut, mk, mke, mv, mve, kb, vb, d_out, fl))
 
     # oracle merge on the host, and the check
     import oracle_ffi
@@ -125,9 +129,10 @@ def main():
     print(json.dumps({
         "what": "compaction replay: decode 1+%d C4 tables -> merge (2 runs) -> encode" % nbot,
         "input_table_bytes": in_bytes, "entries_in": n_in, "entries_out": n_out,
-        "decode_ms": round(t_dec, 4), "merge_ms": round(t_merge, 4), "encode_ms": round(t_enc, 4),
-        "total_ms": round(t_dec + t_merge + t_enc, 4),
-        "input_gibs": round(in_bytes / ((t_dec + t_merge + t_enc) / 1e3) / (1 << 30), 2),
+        "output_tables": ntab_out, "output_bytes": out_bytes,
+        "decode_ms": round(t_dec, 4), "merge_ms": round(t_merge, 4), "cut_ms": round(t_cut, 4),
+        "encode_ms": round(t_enc, 4), "total_ms": round(t_dec + t_merge + t_cut + t_enc, 4),
+        "input_gibs": round(in_bytes / ((t_dec + t_merge + t_cut + t_enc) / 1e3) / (1 << 30), 2),
         "cpu_oracle_merge_ms": round(cpu_merge_s * 1e3, 1),
         "merge_matches_oracle": bool(ok)}))
     codec.close()
