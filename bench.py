@@ -258,10 +258,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # rehearsal only (a one-GPU box): BENCH_DEVICE_OVERRIDE puts every rank on one device and
+    # BENCH_DIST_BACKEND=gloo replaces RCCL, which refuses two ranks on one GPU
+    if os.environ.get("BENCH_DEVICE_OVERRIDE"):
+        local = int(os.environ["BENCH_DEVICE_OVERRIDE"])
     if world > 1:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            tdist.init_process_group(backend)
         dist = tdist
     else:
         torch.cuda.set_device(0)
