@@ -283,12 +283,14 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   uint8_t* kbase = p.key_data ? p.key_data + ek : nullptr;
   uint8_t* vbase = p.val_data ? p.val_data + ev : nullptr;
   // lanes per entry from this block's average entry (known after the walk): 8 for C2-like
-  // 119-B entries, 16 above 128 B (C5 Zipf keys: 0.96 vs 1.10 ms); p.wj forces 8 or 16
+  // 119-B entries, 16 above 128 B (C5 Zipf keys: 0.96 vs 1.10 ms); p.wj forces 8 or 16.
+  // 8 lanes x 5 groups = 40 entries per trip: every C2 block (31-37 entries) in one trip
+  // (same-box A/B vs 4 groups: 0.799 -> 0.781 ms)
   const uint32_t avg = (K + V) / n;
   if (p.wj == 16 || (p.wj == 0 && avg > 128))
     copy_entries<16, 2>(p, meta, blk, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane);
   else
-    copy_entries<8, 4>(p, meta, blk, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane);
+    copy_entries<8, 5>(p, meta, blk, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane);
 }
 
 
