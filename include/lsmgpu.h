@@ -205,6 +205,7 @@ int lsmgpu_open_tables_async(lsmgpu_ctx* ctx, const uint8_t* d_data, uint64_t da
 #define LSMGPU_MERGE_UNSORTED 1
 #define LSMGPU_MERGE_KEY_LEN 2
 #define LSMGPU_MERGE_CAPACITY 4
+#define LSMGPU_MERGE_TIMEOUT 8   /* look-back did not converge (never on a healthy device) */
 typedef struct {
   const uint8_t* key_data;
   const uint32_t* key_end;   /* running end offsets over all runs (key i = [key_end[i-1], key_end[i])) */

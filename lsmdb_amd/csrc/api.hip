@@ -59,7 +59,7 @@ struct lsmgpu_ctx {
   DevBuf scan_tmp;
   DevBuf wsc;            // walk-scan-copy decode scratch (metadata, per-block triples)
   DevBuf open_tmp;       // batched table open: per-table scratch + scan temporary storage
-  DevBuf merge_tmp;      // k-way merge: permutation, triples, scan, flags, scan storage
+  DevBuf merge_tmp;      // k-way merge: permutation, flags, tile bases, splitters
   // staging for host-memory calls
   DevBuf s_data, s_off, s_len, s_kd, s_ke, s_vd, s_ve, s_view, s_bf, s_bs, s_a, s_b, s_c, s_d;
 };
@@ -631,15 +631,23 @@ int lsmgpu_merge_runs_async(lsmgpu_ctx* c, const lsmgpu_runs* in, const lsmgpu_m
   HIPC(hipMemsetAsync(d_result, 0, 8 * sizeof(uint64_t), c->stream));
   const uint32_t n = (uint32_t)in->n;
   auto al = [](size_t b) { return (b + 255) / 256 * 256; };
-  const size_t dst_b = al((size_t)n * 4 + 4), tri_b = al((size_t)n * 24 + 24), flg_b = 256;
+  const size_t dst_b = al((size_t)n * 4 + 4), flg_b = 256;
   const size_t tb_b = al(((size_t)in->nruns + 1) * 4);
   const size_t spl_b = al(((size_t)n / 256 + in->nruns) * in->nruns * 4 + 4);
-  const size_t sbytes = merge_scan_bytes(n ? n : 1);
-  const size_t need = dst_b + 2 * tri_b + flg_b + tb_b + spl_b + sbytes;
+  const size_t need = dst_b + flg_b + tb_b + spl_b;
   if (need > c->merge_tmp.cap) {
     HIPC(hipStreamSynchronize(c->stream));
     HIPC(c->merge_tmp.ensure(need));
   }
+  // emit tile records share the decode's look-back scratch (epoch-tagged, stream-ordered):
+  // [ticket u32, padded to 256 B][64 B per tile]
+  const size_t lb_need = 256 + ((size_t)n / kMergeEmitTile + 1) * 64;
+  if (lb_need > c->lb.cap) {
+    HIPC(hipStreamSynchronize(c->stream));
+    HIPC(c->lb.ensure(lb_need));
+    HIPC(hipMemset(c->lb.p, 0, c->lb.cap));
+  }
+  next_tag(c, 0);
   uint8_t* w = c->merge_tmp.as<uint8_t>();
   MergeParams p{};
   p.kd = in->key_data;
@@ -650,11 +658,12 @@ int lsmgpu_merge_runs_async(lsmgpu_ctx* c, const lsmgpu_runs* in, const lsmgpu_m
   p.nruns = in->nruns;
   p.n = n;
   p.dst = reinterpret_cast<uint32_t*>(w);
-  p.tri = reinterpret_cast<uint64_t*>(w + dst_b);
-  p.base = reinterpret_cast<uint64_t*>(w + dst_b + tri_b);
-  p.flags = reinterpret_cast<uint32_t*>(w + dst_b + 2 * tri_b);
-  p.tile_base = reinterpret_cast<uint32_t*>(w + dst_b + 2 * tri_b + flg_b);
-  p.spl = reinterpret_cast<uint32_t*>(w + dst_b + 2 * tri_b + flg_b + tb_b);
+  p.flags = reinterpret_cast<uint32_t*>(w + dst_b);
+  p.tile_base = reinterpret_cast<uint32_t*>(w + dst_b + flg_b);
+  p.spl = reinterpret_cast<uint32_t*>(w + dst_b + flg_b + tb_b);
+  p.gcnt = c->lb.as<uint32_t>();
+  p.lb = reinterpret_cast<uint64_t*>(c->lb.as<uint8_t>() + 256);
+  p.tag = c->tag;
   p.okd = out->key_data;
   p.key_cap = out->key_cap;
   p.oke = out->key_end;
@@ -664,7 +673,7 @@ int lsmgpu_merge_runs_async(lsmgpu_ctx* c, const lsmgpu_runs* in, const lsmgpu_m
   p.osrc = out->src;
   p.ent_cap = out->ent_cap;
   p.result = d_result;
-  HIPC(launch_merge(p, w + dst_b + 2 * tri_b + flg_b + tb_b + spl_b, sbytes, c->stream));
+  HIPC(launch_merge(p, c->stream));
   return LSMGPU_OK;
 }
 

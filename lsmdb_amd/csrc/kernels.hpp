@@ -122,8 +122,9 @@ struct MergeParams {
   uint32_t nruns;
   uint32_t n;                 // entries (run_first[nruns])
   uint32_t* dst;              // scratch: merged position -> entry
-  uint64_t* tri;              // scratch: n x {keep, key bytes, value bytes}
-  uint64_t* base;             // scratch: their exclusive scan
+  uint32_t* gcnt;             // emit tile ticket (0 between launches, reset by the last ticket)
+  uint64_t* lb;               // emit tile records (64 B per tile, epoch-tagged)
+  uint64_t tag;
   uint32_t* flags;            // scratch: [0] input errors, [1] capacity
   uint32_t* tile_base;        // scratch: nruns + 1
   uint32_t* spl;              // scratch: (n / 256 + nruns) x nruns splitter ranks
@@ -137,8 +138,8 @@ struct MergeParams {
   uint64_t ent_cap;
   uint64_t* result;
 };
-size_t merge_scan_bytes(uint32_t n);
-hipError_t launch_merge(const MergeParams& p, void* scan_tmp, size_t scan_bytes, hipStream_t s);
+constexpr uint32_t kMergeEmitTile = 1024;  // merged positions per emit workgroup
+hipError_t launch_merge(const MergeParams& p, hipStream_t s);
 
 // launchers (return hipError_t)
 hipError_t launch_decode(const DecodeParams& p, uint32_t max_blk_len, int num_cus,

@@ -14,32 +14,22 @@
 //                           tile's splitters (ranks are monotone in a sorted run), upper bound
 //                           for lower-index runs (equal keys of a lower nice come first),
 //                           lower bound for higher-index runs
-//   keep   (lane = merged position)  first of its equal-key group (bytes.Equal with the
-//                           predecessor, y/iterator.go:172-181)
-//   scan   (rocPRIM)        output entry index, key and value byte offsets of the kept entries
-//   gather (8 lanes / entry) 16-B piece copies of key and raw vs-enc bytes, end offsets, source
+//   emit   (lane = 4 merged positions, workgroup = 1024)  keep = first of its equal-key
+//                           group (bytes.Equal with the predecessor, y/iterator.go:172-181);
+//                           the tile's scan of {kept, key bytes, value bytes} and its output
+//                           base by decoupled look-back; end offsets, source index, and 8 lanes
+//                           per kept entry copy 16-B pieces of key and raw vs-enc bytes
 // Unsorted runs (the heap would interleave them differently) and keys <= 8 B are reported in
 // result[3] and produce no output.
-#include <rocprim/device/device_scan.hpp>
-
-#include "codec_common.hpp"
+#include "decode_common.hpp"
 #include "kernels.hpp"
 
 namespace lsmgpu {
 
 namespace {
 
-constexpr uint32_t M_UNSORTED = 1, M_KEY_LEN = 2, M_CAPACITY = 4;
+constexpr uint32_t M_UNSORTED = 1, M_KEY_LEN = 2, M_CAPACITY = 4, M_TIMEOUT = 8;
 constexpr uint32_t kMergeTile = 256;  // entries per splitter tile
-
-struct MTri {
-  uint64_t n, k, v;
-};
-struct MTriPlus {
-  __device__ __host__ MTri operator()(const MTri& a, const MTri& b) const {
-    return MTri{a.n + b.n, a.k + b.k, a.v + b.v};
-  }
-};
 
 __device__ __forceinline__ const uint8_t* key_of(const MergeParams& p, uint32_t i, uint32_t& len) {
   const uint32_t s = i ? p.ke[i - 1] : 0u;
@@ -137,76 +127,184 @@ __global__ void merge_rank_kernel(MergeParams p) {
   p.dst[pos] = i;
 }
 
-__global__ void merge_keep_kernel(MergeParams p) {
-  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= p.n) return;
-  MTri t{0, 0, 0};
-  if (!*p.flags) {
-    const uint32_t i = p.dst[q];
-    uint32_t li;
-    const uint8_t* ki = key_of(p, i, li);
-    bool keep = true;
-    if (q > 0) {  // bytes.Equal(key, curKey): the merged predecessor is the last candidate
-      uint32_t lp;
-      const uint8_t* kp = key_of(p, p.dst[q - 1], lp);
-      if (lp == li) keep = bytes_compare(kp, lp, ki, li) != 0;
-    }
-    if (keep) t = MTri{1, li, (uint64_t)(p.ve[i] - (i ? p.ve[i - 1] : 0u))};
-  }
-  reinterpret_cast<MTri*>(p.tri)[q] = t;
-}
+// keep + scan + gather in one pass (lane = 4 consecutive merged positions, a workgroup = a
+// tile of kEmitTile positions taken by ticket): an entry is kept unless its key equals its
+// merged predecessor's (bytes.Equal with the last candidate, y/iterator.go:172-181); the
+// tile scans {kept, key bytes, value bytes}, finds its output base by decoupled look-back
+// over the tile records (epoch-tagged granules in p.lb, as in the decode walk), writes the
+// end offsets and source index of its kept entries, then 8 lanes per kept entry copy the key
+// and raw vs-enc bytes as 16-B pieces.  No permutation-sized scratch beyond dst.
+constexpr uint32_t kEmitTile = kMergeEmitTile;
 
-// 8 lanes per merged position
-__global__ void __launch_bounds__(256) merge_gather_kernel(MergeParams p) {
-  constexpr uint32_t J = 8;
-  const uint32_t lane = threadIdx.x & (J - 1);
-  const uint32_t q = (blockIdx.x * blockDim.x + threadIdx.x) / J;
-  if (q >= p.n || *p.flags) return;
-  const MTri t = reinterpret_cast<const MTri*>(p.tri)[q];
-  const MTri b = reinterpret_cast<const MTri*>(p.base)[q];
-  if (q == p.n - 1 && lane == 0) {  // totals
-    p.result[0] = b.n + t.n;
-    p.result[1] = b.k + t.k;
-    p.result[2] = b.v + t.v;
-    if (b.n + t.n > p.ent_cap || (p.okd && b.k + t.k > p.key_cap) ||
-        (p.ovd && b.v + t.v > p.val_cap) || b.k + t.k > 0xffffffffull || b.v + t.v > 0xffffffffull)
-      atomicOr(p.flags + 1, M_CAPACITY);
+__device__ __forceinline__ uint4 load16u(const uint8_t* p) {  // any alignment
+  uint4 v;
+  __builtin_memcpy(&v, p, 16);
+  return v;
+}
+__device__ __forceinline__ void store16u(uint8_t* p, uint4 v) { __builtin_memcpy(p, &v, 16); }
+
+__global__ void __launch_bounds__(256) merge_emit_kernel(MergeParams p) {
+  __shared__ uint4 s_ent[kEmitTile][2];  // kept entries: {i, ks, kl, bk}, {vs, vl, bv, bn}
+  __shared__ uint32_t s_tile;
+  __shared__ uint32_t s_wave[4][3];
+  __shared__ uint32_t s_ex[3];
+  if (p.flags[0]) return;  // input errors (stream-ordered before this launch): no output
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint32_t ntiles = (p.n + kEmitTile - 1) / kEmitTile;
+  if (tid == 0) {
+    const uint32_t t = atomicAdd(p.gcnt, 1u);
+    if (t == ntiles - 1) atomicExch(p.gcnt, 0u);  // every ticket is taken
+    s_tile = t;
   }
-  if (!t.n) return;
-  if (b.n >= p.ent_cap || (p.okd && b.k + t.k > p.key_cap) || (p.ovd && b.v + t.v > p.val_cap))
-    return;
-  const uint32_t i = p.dst[q];
-  const uint32_t ks = i ? p.ke[i - 1] : 0u, vs = i ? p.ve[i - 1] : 0u;
-  const uint32_t kl = (uint32_t)t.k, vl = (uint32_t)t.v;
-  if (lane == 0) {
-    if (p.oke) p.oke[b.n] = (uint32_t)(b.k + kl);
-    if (p.ove) p.ove[b.n] = (uint32_t)(b.v + vl);
-    if (p.osrc) p.osrc[b.n] = i;
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  const uint32_t q0 = tile * kEmitTile + 4 * tid;
+  uint32_t src[4], kl[4], vl[4], ks[4], vs[4];
+  uint32_t keepm = 0, tn = 0, tk = 0, tv = 0;
+  if (q0 < p.n) {
+    if (q0 + 4 <= p.n) {
+      const uint4 d = *reinterpret_cast<const uint4*>(p.dst + q0);
+      src[0] = d.x; src[1] = d.y; src[2] = d.z; src[3] = d.w;
+    } else {
+      for (uint32_t c = 0; c < 4; c++) src[c] = q0 + c < p.n ? p.dst[q0 + c] : 0u;
+    }
+    uint32_t lp = 0;
+    const uint8_t* kp = nullptr;
+    if (q0 > 0) kp = key_of(p, p.dst[q0 - 1], lp);
+    for (uint32_t c = 0; c < 4; c++) {
+      if (q0 + c >= p.n) { kl[c] = vl[c] = ks[c] = vs[c] = 0; continue; }
+      const uint32_t i = src[c];
+      ks[c] = i ? p.ke[i - 1] : 0u;
+      vs[c] = i ? p.ve[i - 1] : 0u;
+      kl[c] = p.ke[i] - ks[c];
+      vl[c] = p.ve[i] - vs[c];
+      const uint8_t* ki = p.kd + ks[c];
+      const bool keep = !kp || lp != kl[c] || bytes_compare(kp, lp, ki, kl[c]) != 0;
+      if (keep) {
+        keepm |= 1u << c;
+        tn++;
+        tk += kl[c];
+        tv += vl[c];
+      }
+      kp = ki;
+      lp = kl[c];
+    }
   }
-  const uint32_t kp = p.okd ? pieces16(kl) : 0u, np = kp + (p.ovd ? pieces16(vl) : 0u);
-  for (uint32_t c = lane; c < np; c += J) {
-    const bool key = c < kp;
-    copy_piece16(key ? p.okd + b.k : p.ovd + b.v, key ? p.kd + ks : p.vd + vs, key ? kl : vl,
-                 key ? c : c - kp);
+  // tile scan (u32: kept key / value bytes are bounded by the <= 4 GiB - 1 input streams)
+  const uint32_t in_ = wave_scan_sat(tn, lane), ik = wave_scan_sat(tk, lane),
+                 iv = wave_scan_sat(tv, lane);
+  if (lane == 63) {
+    s_wave[wave][0] = in_;
+    s_wave[wave][1] = ik;
+    s_wave[wave][2] = iv;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    uint32_t an = 0, ak = 0, av = 0;
+    for (int w = 0; w < 4; w++) {
+      an = sat_add(an, s_wave[w][0]);
+      ak = sat_add(ak, s_wave[w][1]);
+      av = sat_add(av, s_wave[w][2]);
+    }
+    uint64_t* R = p.lb + (uint64_t)tile * 8;
+    Tot ex{0, 0, 0};
+    if (tile > 0) {
+      store3(R, p.tag, an, ak, av, lane);
+      ex = lookback(p.lb, tile, p.tag, lane, p.result);
+    }
+    store3(R + 4, p.tag, sat_add(ex.n, an), sat_add(ex.k, ak), sat_add(ex.v, av), lane);
+    if (lane == 0) {
+      s_ex[0] = ex.n;
+      s_ex[1] = ex.k;
+      s_ex[2] = ex.v;
+      if (tile == ntiles - 1) {  // totals (the last tile's inclusive prefix)
+        const uint64_t N = sat_add(ex.n, an), K = sat_add(ex.k, ak), V = sat_add(ex.v, av);
+        p.result[0] = N;
+        p.result[1] = K;
+        p.result[2] = V;
+        if (N > p.ent_cap || (p.okd && K > p.key_cap) || (p.ovd && V > p.val_cap))
+          atomicOr(p.flags + 1, M_CAPACITY);
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t ln = in_ - tn, bk = ik - tk, bv = iv - tv;  // exclusive inside the wave
+  uint32_t wn = 0;                                       // tile-local entry index base
+  for (uint32_t w = 0; w < wave; w++) {
+    wn += s_wave[w][0];
+    bk += s_wave[w][1];
+    bv += s_wave[w][2];
+  }
+  ln += wn;
+  bk += s_ex[1];
+  bv += s_ex[2];
+  const uint32_t n0 = s_ex[0];
+  for (uint32_t c = 0; c < 4; c++) {
+    if (!((keepm >> c) & 1u)) continue;
+    const uint32_t bn = n0 + ln;
+    s_ent[ln][0] = make_uint4(src[c], ks[c], kl[c], bk);
+    s_ent[ln][1] = make_uint4(vs[c], vl[c], bv, bn);
+    const bool fits = bn < p.ent_cap && !(p.okd && (uint64_t)bk + kl[c] > p.key_cap) &&
+                      !(p.ovd && (uint64_t)bv + vl[c] > p.val_cap);
+    if (fits) {
+      if (p.oke) p.oke[bn] = bk + kl[c];
+      if (p.ove) p.ove[bn] = bv + vl[c];
+      if (p.osrc) p.osrc[bn] = src[c];
+    }
+    ln++;
+    bk += kl[c];
+    bv += vl[c];
+  }
+  __syncthreads();
+  // gather: 8 lanes per kept entry, kGatherG entries per lane per trip with every first-round
+  // 16-B piece loaded before any is stored (more loads in flight per wave)
+  constexpr uint32_t kGatherG = 4;
+  const uint32_t m = s_wave[0][0] + s_wave[1][0] + s_wave[2][0] + s_wave[3][0];
+  const uint32_t sub = tid & 7u;
+  for (uint32_t e0 = tid >> 3; e0 < m; e0 += kGatherG * (256 / 8)) {
+    uint4 v[kGatherG];
+    uint8_t* d[kGatherG];
+#pragma unroll
+    for (uint32_t g = 0; g < kGatherG; g++) {
+      d[g] = nullptr;
+      const uint32_t e = e0 + g * (256 / 8);
+      if (e >= m) continue;
+      const uint4 a = s_ent[e][0], b = s_ent[e][1];
+      const uint32_t eks = a.y, ekl = a.z, ebk = a.w, evs = b.x, evl = b.y, ebv = b.z, ebn = b.w;
+      if (ebn >= p.ent_cap || (p.okd && (uint64_t)ebk + ekl > p.key_cap) ||
+          (p.ovd && (uint64_t)ebv + evl > p.val_cap))
+        continue;
+      const uint32_t kpc = p.okd ? pieces16(ekl) : 0u, np = kpc + (p.ovd ? pieces16(evl) : 0u);
+      for (uint32_t c = sub; c < np; c += 8) {
+        const bool key = c < kpc;
+        uint8_t* dst = key ? p.okd + ebk : p.ovd + ebv;
+        const uint8_t* src = key ? p.kd + eks : p.vd + evs;
+        const uint32_t len = key ? ekl : evl, q = key ? c : c - kpc;
+        if (c == sub && len >= 16) {  // first round: deferred store
+          const uint32_t o = min(16 * q, len - 16);
+          v[g] = load16u(src + o);
+          d[g] = dst + o;
+        } else {
+          copy_piece16(dst, src, len, q);
+        }
+      }
+    }
+#pragma unroll
+    for (uint32_t g = 0; g < kGatherG; g++)
+      if (d[g]) store16u(d[g], v[g]);
   }
 }
 
 __global__ void merge_flags_kernel(MergeParams p) {
-  if (threadIdx.x == 0) p.result[3] = (uint64_t)(p.flags[0] | p.flags[1]);
+  if (threadIdx.x == 0)
+    p.result[3] = (uint64_t)(p.flags[0] | p.flags[1]) | (p.result[5] ? M_TIMEOUT : 0u);
 }
 
-size_t merge_scan_bytes(uint32_t n) {
-  size_t bytes = 0;
-  (void)rocprim::exclusive_scan(nullptr, bytes, (const MTri*)nullptr, (MTri*)nullptr,
-                                MTri{0, 0, 0}, (size_t)n, MTriPlus());
-  return bytes;
-}
-
-hipError_t launch_merge(const MergeParams& p, void* scan_tmp, size_t scan_bytes, hipStream_t s) {
+hipError_t launch_merge(const MergeParams& p, hipStream_t s) {
   hipError_t e;
   if ((e = hipMemsetAsync(p.flags, 0, 8, s)) != hipSuccess) return e;
   if (p.n) {
-    const dim3 g((p.n + 255) / 256), g8((uint32_t)(((uint64_t)p.n * 8 + 255) / 256));
+    const dim3 g((p.n + 255) / 256);
     hipLaunchKernelGGL(merge_check_kernel, g, dim3(256), 0, s, p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(merge_tiles_kernel, dim3(1), dim3(64), 0, s, p);
@@ -217,14 +315,8 @@ hipError_t launch_merge(const MergeParams& p, void* scan_tmp, size_t scan_bytes,
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(merge_rank_kernel, g, dim3(256), 0, s, p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(merge_keep_kernel, g, dim3(256), 0, s, p);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    size_t bytes = scan_bytes;
-    e = rocprim::exclusive_scan(scan_tmp, bytes, reinterpret_cast<const MTri*>(p.tri),
-                                reinterpret_cast<MTri*>(p.base), MTri{0, 0, 0}, (size_t)p.n,
-                                MTriPlus(), s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(merge_gather_kernel, g8, dim3(256), 0, s, p);
+    hipLaunchKernelGGL(merge_emit_kernel, dim3((p.n + kEmitTile - 1) / kEmitTile), dim3(256), 0,
+                       s, p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   hipLaunchKernelGGL(merge_flags_kernel, dim3(1), dim3(64), 0, s, p);
