@@ -165,6 +165,9 @@ class Codec:
         nblk = off.size
         key_cap = val_cap = max(int(buf.size), 16)
         ent_cap = max(int(ln.astype(np.uint64).sum()) // 10 + 1, 1)
+        # MODE_VIEW alone: the view index only (key/value arrays come back empty); any other
+        # mode also materializes, so the HostDecoded accessors work
+        eff = mode if mode == MODE_VIEW else mode | MODE_MATERIALIZE
         for _attempt in range(2):
             kd = np.zeros(key_cap, dtype=np.uint8)
             vd = np.zeros(val_cap, dtype=np.uint8)
@@ -179,7 +182,7 @@ class Codec:
             d.view, d.ent_cap = _ptr(vw), ent_cap
             d.blk_first, d.blk_status = _ptr(bf), _ptr(bs)
             rc = lib().lsmgpu_decode_blocks(self._ctx, _ptr(buf), buf.size, 0, _ptr(off), _ptr(ln),
-                                            nblk, mode | MODE_MATERIALIZE, byref(d))
+                                            nblk, eff, byref(d))
             if rc == _lib.ERR_CAPACITY:  # plen>0 blocks can expand keys: retry with exact sizes
                 key_cap = max(int(d.key_bytes), 16)
                 val_cap = max(int(d.val_bytes), 16)

@@ -264,6 +264,9 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     const char* j_env = getenv("LSMGPU_WSC_J");  // A/B: lanes per entry in the copy
     p.wj = j_env ? (uint32_t)atoi(j_env) : 0u;
     if (p.wj != 8 && p.wj != 16) p.wj = 0;
+    // view-only decode finishes inside the walk (LSMGPU_WSC_VIEWFUSE=0: separate copy launch)
+    const char* vf_env = getenv("LSMGPU_WSC_VIEWFUSE");
+    p.wfuse = !(mode & LSMGPU_MODE_MATERIALIZE) && !(vf_env && atoi(vf_env) == 0);
     HIPC(launch_decode_wsc(p, c->stream));
     return LSMGPU_OK;
   }

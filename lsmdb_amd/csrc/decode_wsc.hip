@@ -73,6 +73,8 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   __shared__ uint32_t s_tile;
   __shared__ uint32_t s_wave[4][3];
   __shared__ uint32_t s_ex[3];
+  __shared__ uint32_t s_first[257];  // p.wfuse: tile-relative first entry of each block
+  __shared__ uint32_t s_off[256];    // p.wfuse: each block's input offset
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t ntiles = (p.nblk + 255) / 256;
   if (tid == 0) {
@@ -83,11 +85,12 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   __syncthreads();
   const uint32_t tile = s_tile;
   const uint32_t b = tile * 256 + tid;
-  uint32_t n = 0, K = 0, V = 0;
+  uint32_t n = 0, K = 0, V = 0, st = LSMGPU_BLK_OK;
   if (b < p.nblk) {
     uint2* row = stage + tid * kWalkStage;
     const uint32_t off = p.blk_off[b], len = p.blk_len[b];
-    uint32_t st = LSMGPU_BLK_OK, pos = 0;
+    uint32_t pos = 0;
+    s_off[tid] = off;
     uint2* meta = reinterpret_cast<uint2*>(p.wmeta) + (uint64_t)b * p.wcap;
     if ((uint64_t)off + len > p.data_len) {
       st = LSMGPU_BLK_RANGE;
@@ -156,10 +159,60 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
       ok = sat_add(ok, s_wave[w][1]);
       ov = sat_add(ov, s_wave[w][2]);
     }
-    uint64_t* bs = p.wbase + 3ull * b;
-    bs[0] = sat_add(on, in_ - n);
-    bs[1] = sat_add(ok, ik == 0xffffffffu ? ik : ik - K);
-    bs[2] = sat_add(ov, iv - V);
+    const uint32_t en = sat_add(on, in_ - n), ek = sat_add(ok, ik == 0xffffffffu ? ik : ik - K),
+                   ev = sat_add(ov, iv - V);
+    if (!p.wfuse) {
+      uint64_t* bs = p.wbase + 3ull * b;
+      bs[0] = en;
+      bs[1] = ek;
+      bs[2] = ev;
+    } else {  // view-only decode: the copy kernel's per-block duties, done here
+      if (p.blk_first) p.blk_first[b] = en;
+      if (p.blk_status) p.blk_status[b] = (int32_t)st;
+      if (st != LSMGPU_BLK_OK) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(p.result + 4), 1ull);
+        atomicMax(reinterpret_cast<unsigned long long*>(p.result + 3),
+                  (unsigned long long)(p.nblk - b));
+      }
+      if (b == p.nblk - 1) {  // totals of the whole batch
+        if (p.blk_first) p.blk_first[p.nblk] = (uint32_t)((uint64_t)en + n);
+        p.result[0] = (uint64_t)en + n;
+        p.result[1] = (uint64_t)ek + K;
+        p.result[2] = (uint64_t)ev + V;
+      }
+      if (!((uint64_t)en + n <= p.ent_cap && (uint64_t)en + n <= 0xffffffffull))
+        atomicOr(reinterpret_cast<unsigned long long*>(p.result + 5), 1ull);
+    }
+  }
+  if (!p.wfuse) return;
+  // View-only decode (p.wfuse): the workgroup writes its tile's dense view records itself, so
+  // no copy launch follows.  Output entry e of the tile belongs to the last block whose first
+  // entry is <= e (binary search over s_first); its record comes from the walk metadata this
+  // workgroup just wrote (L2-hot), and consecutive threads write consecutive 8-B records.
+  {
+    uint32_t rel = in_ - n;  // entries of the tile never saturate (<= 256 x 6,554)
+    for (uint32_t w = 0; w < wave; w++) rel += s_wave[w][0];
+    s_first[tid] = rel;
+    if (tid == 255) s_first[256] = rel + n;
+  }
+  __syncthreads();
+  if (!p.view || (p.ablate & 2)) return;
+  const uint32_t nt = s_first[256];
+  const uint64_t e0 = s_ex[0];
+  for (uint32_t e = tid; e < nt; e += 256) {
+    uint32_t lo = 0, hi = 255;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (s_first[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    const uint64_t bend = e0 + s_first[lo + 1];
+    if (bend > p.ent_cap || bend > 0xffffffffull) continue;  // reported above (result[5])
+    const uint32_t i = e - s_first[lo];
+    const uint2* meta = reinterpret_cast<const uint2*>(p.wmeta) + (uint64_t)(tile * 256 + lo) * p.wcap;
+    const uint2 m0 = meta[i], m1 = meta[i + 1];
+    const uint32_t hp = m0.x & 0xffffu, vl = (m1.x >> 16) - (m0.x >> 16);
+    const uint32_t kl = (m1.x & 0xffffu) - hp - 10 - vl;  // stored key bytes
+    p.view[e0 + e] = (uint64_t)(s_off[lo] + hp + 10) | ((uint64_t)kl << 32) | ((uint64_t)vl << 48);
   }
 }
 
@@ -591,7 +644,7 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s) {
   const uint32_t nblk = p.nblk;
   hipLaunchKernelGGL(wsc_walk_kernel, dim3((nblk + 255) / 256), dim3(256), 0, s, p);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  if (e != hipSuccess || p.wfuse) return e;  // view-only: the walk wrote everything
   const uint32_t per_wg = 4 / p.wsplit;  // blocks per 4-wave workgroup
   hipLaunchKernelGGL(wsc_copy_kernel, dim3((nblk + per_wg - 1) / per_wg), dim3(256), 0, s, p);
   return hipGetLastError();

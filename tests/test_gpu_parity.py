@@ -315,6 +315,42 @@ def test_forced_decode_paths(codec, oracle, monkeypatch, path):
     test_prefix_compressed_random(codec, oracle)
 
 
+@pytest.mark.parametrize("fuse", ["1", "0"])
+def test_wsc_view_only(codec, oracle, monkeypatch, fuse):
+    """View-only decode on walk-scan-copy: the walk writes the dense view index, blk_first,
+    blk_status and the totals itself (LSMGPU_WSC_VIEWFUSE=1, the default) or leaves them to the
+    copy launch (=0).  C2 4 KiB blocks, C5 Zipf 32 KiB blocks, short random entries, every KAT
+    block (error statuses, terminators, plen > 0) at odd alignments."""
+    from lsmdb_amd.codec import MODE_VIEW
+    monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
+    monkeypatch.setenv("LSMGPU_WSC_VIEWFUSE", fuse)
+    c2 = _cols(2, 30000, seed=3)
+    c5 = _cols(5, 20000, seed=9)
+    parts = [oracle.build_cols(c2.keys, c2.key_end, c2.vs, c2.vs_end, 0, 4096)[0],
+             oracle.build_cols(c5.keys, c5.key_end, c5.vs, c5.vs_end, c5.entries_per_block,
+                               c5.block_bytes)[0],
+             oracle.build_cols(*_random_cols(20000, 5), 0, 4096)[0]]
+    data, off, ln = _sst_blocks(oracle, parts)
+    kd = bytearray(data)
+    offs, lens = list(off), list(ln)
+    for i, (_n, block, _e, _s) in enumerate(K.DECODE_KATS * 3):
+        kd += b"\xab" * (i % 13)
+        offs.append(len(kd))
+        lens.append(len(block))
+        kd += block
+    kd = bytes(kd)
+    o2, l2 = np.array(offs, np.uint32), np.array(lens, np.uint32)
+    for sl in (slice(None), slice(0, 300), slice(len(off) - 5, None)):
+        g = codec.decode_host(kd, o2[sl], l2[sl], mode=MODE_VIEW)
+        o = oracle.decode(kd, o2[sl], l2[sl])
+        assert g.n_entries == o.n_entries
+        assert np.array_equal(g.view, o.view)
+        assert np.array_equal(g.blk_first, o.blk_first)
+        assert np.array_equal(g.blk_status, o.blk_status)
+        assert g.first_bad_block == o.first_bad_block
+        assert g.n_bad_blocks == o.n_bad_blocks
+
+
 @pytest.mark.parametrize("split", [1, 2, 4])
 def test_wsc_split(codec, oracle, monkeypatch, split):
     """Walk-scan-copy with 1, 2 or 4 waves sharing each block's copy (LSMGPU_WSC_SPLIT): C5
