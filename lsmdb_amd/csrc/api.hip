@@ -264,9 +264,13 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     const char* j_env = getenv("LSMGPU_WSC_J");  // A/B: lanes per entry in the copy
     p.wj = j_env ? (uint32_t)atoi(j_env) : 0u;
     if (p.wj != 8 && p.wj != 16) p.wj = 0;
-    // view-only decode finishes inside the walk (LSMGPU_WSC_VIEWFUSE=0: separate copy launch)
+    // view-only decode finishes inside the walk when there are >= 2 walk tiles (256 blocks)
+    // per CU; with fewer, the tile epilogues run on too few workgroups and the copy launch wins
+    // (measured: C2 1 GiB 0.413 -> 0.323 ms fused; C4 64 MiB, 21 tiles: 0.085 -> 0.165 ms).
+    // LSMGPU_WSC_VIEWFUSE=1 / 0 forces it on / off.
     const char* vf_env = getenv("LSMGPU_WSC_VIEWFUSE");
-    p.wfuse = !(mode & LSMGPU_MODE_MATERIALIZE) && !(vf_env && atoi(vf_env) == 0);
+    const bool fuse = vf_env ? atoi(vf_env) != 0 : nblk >= 512ull * (uint64_t)c->num_cus;
+    p.wfuse = !(mode & LSMGPU_MODE_MATERIALIZE) && fuse;
     HIPC(launch_decode_wsc(p, c->stream));
     return LSMGPU_OK;
   }
