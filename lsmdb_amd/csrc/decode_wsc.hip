@@ -225,17 +225,29 @@ __device__ __forceinline__ void copy_entries(const DecodeParams& p, const uint2*
                                              const uint8_t* blk, uint8_t* kbase, uint8_t* vbase,
                                              uint32_t n, uint64_t en, uint64_t ek, uint64_t ev,
                                              uint32_t off, uint32_t sub, uint32_t split,
-                                             bool mat, bool view, uint32_t lane) {
+                                             bool mat, bool view, uint32_t lane, uint2 pre) {
   const uint32_t j = lane & (J - 1);
   bool any_plen = false;
   for (uint32_t e0 = sub * G * (kWave / J); e0 < n; e0 += split * G * (kWave / J)) {
     uint32_t hp[G], kl[G], vl[G], ko[G], vo[G], np[G], kp[G];
     bool on[G];
+    // a pass whose entries (and their successors) are all below 64 reads the metadata the
+    // kernel preloaded one record per lane (`pre`) by lane shuffle, not from memory
+    const bool shuffled = e0 + G * (kWave / J) < kWave;
 #pragma unroll
     for (int i = 0; i < G; i++) {
       const uint32_t e = e0 + i * (kWave / J) + (lane / J);
       const uint32_t ec = min(e, n - 1);
-      const uint2 m0 = meta[ec], m1 = meta[ec + 1];
+      uint2 m0, m1;
+      if (shuffled) {
+        m0.x = (uint32_t)__shfl((int)pre.x, (int)ec);
+        m0.y = (uint32_t)__shfl((int)pre.y, (int)ec);
+        m1.x = (uint32_t)__shfl((int)pre.x, (int)ec + 1);
+        m1.y = (uint32_t)__shfl((int)pre.y, (int)ec + 1);
+      } else {
+        m0 = meta[ec];
+        m1 = meta[ec + 1];
+      }
       hp[i] = m0.x & 0xffffu;
       vo[i] = m0.x >> 16;
       ko[i] = m0.y;
@@ -296,6 +308,10 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   const uint32_t sub = wave % split;
   const uint32_t b = uniform(blockIdx.x * (4 / split) + wave / split);
   if (b >= p.nblk) return;
+  const uint2* meta = reinterpret_cast<const uint2*>(p.wmeta) + (uint64_t)b * p.wcap;
+  // the first 64 metadata records, one per lane, requested beside the per-block loads below
+  // (one round trip fewer before the piece loads; records past the sentinel are never used)
+  const uint2 pre = meta[min(lane, p.wcap - 1)];
   const uint64_t* t = p.wstat + 3ull * b;
   const uint32_t n = uniform((uint32_t)t[0]), K = uniform((uint32_t)t[1]),
                  V = uniform((uint32_t)t[2]);
@@ -332,7 +348,6 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   }
   if (n == 0 || (p.ablate & 2)) return;
   const uint8_t* blk = p.data + off;
-  const uint2* meta = reinterpret_cast<const uint2*>(p.wmeta) + (uint64_t)b * p.wcap;
   uint8_t* kbase = p.key_data ? p.key_data + ek : nullptr;
   uint8_t* vbase = p.val_data ? p.val_data + ev : nullptr;
   // lanes per entry from this block's average entry (known after the walk): 8 for C2-like
@@ -341,9 +356,9 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   // (same-box A/B vs 4 groups: 0.799 -> 0.781 ms)
   const uint32_t avg = (K + V) / n;
   if (p.wj == 16 || (p.wj == 0 && avg > 128))
-    copy_entries<16, 2>(p, meta, blk, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane);
+    copy_entries<16, 2>(p, meta, blk, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
   else
-    copy_entries<8, 5>(p, meta, blk, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane);
+    copy_entries<8, 5>(p, meta, blk, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
 }
 
 
