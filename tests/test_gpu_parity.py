@@ -210,6 +210,42 @@ def test_capacity_overflow_reported(codec, oracle):
     assert res[0] == o.n_entries
 
 
+@pytest.mark.parametrize("fuse", ["1", "0"])
+def test_view_only_capacity_overflow(codec, oracle, monkeypatch, fuse):
+    """View-only decode into a view buffer too small for the batch: the capacity flag is set,
+    the totals stay exact, blocks that fit are written exactly as the oracle's, and nothing is
+    written past ent_cap (sentinel tail) -- with the walk's view epilogue and with the copy."""
+    import torch
+    monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
+    monkeypatch.setenv("LSMGPU_WSC_VIEWFUSE", fuse)
+    c = _cols(2, 40000, seed=5)
+    ref, _, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, 0, 4096)
+    sst = ref + b"{}" + (2).to_bytes(4, "big")
+    off, ln, _, _ = oracle.parse_index(sst)
+    o = oracle.decode(sst, off, ln)
+    dev = torch.device("cuda", 0)
+    d_data = torch.from_numpy(np.frombuffer(sst, np.uint8).copy()).to(dev)
+    d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+    d_len = torch.from_numpy(ln.view(np.int32)).to(dev)
+    cap = o.n_entries // 2 + 7
+    bufs = codec.alloc_decode(len(sst), int(ln.sum()), off.size, 2, ent_cap=cap)
+    sentinel = -0x5A5A5A5A5A5A5A5B
+    bufs.view = torch.full((cap + 4096,), sentinel, dtype=torch.int64, device=dev)
+    bufs.bind()
+    codec.decode_device_async(d_data, d_off, d_len, int(ln.max()), 2, bufs)
+    codec.synchronize()
+    res = bufs.result.cpu().numpy()
+    assert res[5] & 1
+    assert res[0] == o.n_entries
+    view = bufs.view.cpu().numpy()
+    assert (view[cap:] == sentinel).all()
+    assert np.array_equal(bufs.blk_first.cpu().numpy().view(np.uint32), o.blk_first)
+    fit = int(np.searchsorted(o.blk_first[1:], cap, side="right"))  # blocks ending <= cap
+    assert fit > 0
+    end = int(o.blk_first[fit])
+    assert np.array_equal(view[:end].view(np.uint64), o.view[:end])
+
+
 def test_encode_values_gpu(codec, oracle):
     rng = np.random.default_rng(11)
     n = 5000
