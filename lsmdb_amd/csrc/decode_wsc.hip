@@ -199,11 +199,24 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   if (!p.view || (p.ablate & 2)) return;
   const uint32_t nt = s_first[256];
   const uint64_t e0 = s_ex[0];
+  // entry -> block map in the walk's staging rows (free now): each thread marks its block's
+  // entries, so the lookup is one LDS read (tiles of more entries: binary search)
+  uint16_t* owner = reinterpret_cast<uint16_t*>(stage);
+  const bool mapped = nt <= 256 * kWalkStage * 4;  // u16 slots in the staging rows
+  if (mapped) {
+    const uint32_t f = s_first[tid];
+    for (uint32_t i = 0; i < n; i++) owner[f + i] = (uint16_t)tid;
+    __syncthreads();
+  }
   for (uint32_t e = tid; e < nt; e += 256) {
     uint32_t lo = 0, hi = 255;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi + 1) >> 1;
-      if (s_first[mid] <= e) lo = mid; else hi = mid - 1;
+    if (mapped) {
+      lo = owner[e];
+    } else {
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (s_first[mid] <= e) lo = mid; else hi = mid - 1;
+      }
     }
     const uint64_t bend = e0 + s_first[lo + 1];
     if (bend > p.ent_cap || bend > 0xffffffffull) continue;  // reported above (result[5])

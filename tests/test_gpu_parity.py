@@ -365,7 +365,9 @@ def test_wsc_view_only(codec, oracle, monkeypatch, fuse):
     parts = [oracle.build_cols(c2.keys, c2.key_end, c2.vs, c2.vs_end, 0, 4096)[0],
              oracle.build_cols(c5.keys, c5.key_end, c5.vs, c5.vs_end, c5.entries_per_block,
                                c5.block_bytes)[0],
-             oracle.build_cols(*_random_cols(20000, 5), 0, 4096)[0]]
+             oracle.build_cols(*_random_cols(20000, 5), 0, 4096)[0],
+             # ~170 tiny entries per block: tiles of > 17,408 entries (binary-search lookup)
+             oracle.build_cols(*_random_cols(120000, 11, 9, 10, 3, 4), 0, 4096)[0]]
     data, off, ln = _sst_blocks(oracle, parts)
     kd = bytearray(data)
     offs, lens = list(off), list(ln)
@@ -376,7 +378,8 @@ def test_wsc_view_only(codec, oracle, monkeypatch, fuse):
         kd += block
     kd = bytes(kd)
     o2, l2 = np.array(offs, np.uint32), np.array(lens, np.uint32)
-    for sl in (slice(None), slice(0, 300), slice(len(off) - 5, None)):
+    for sl in (slice(None), slice(0, 300), slice(len(off) - 5, None),
+               slice(len(off) - 700, None)):
         g = codec.decode_host(kd, o2[sl], l2[sl], mode=MODE_VIEW)
         o = oracle.decode(kd, o2[sl], l2[sl])
         assert g.n_entries == o.n_entries
