@@ -120,18 +120,35 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
   // the block's last entry writes the terminator and the restart.
   const uint32_t j = lane & (J - 1);
   uint32_t bad = 0, bs = 0, carry = 0;
+  // the starts of the block's first 64 entries, one per lane (key_end / vs_end of entry
+  // f + lane - 1), in one round trip: passes over entries < 63 take offsets by lane shuffle
+  const uint64_t pidx = f + lane;
+  const uint64_t pc = pidx - 1 < p.n - 1 ? pidx - 1 : p.n - 1;
+  const uint32_t pk = pidx ? p.key_end[pc] : 0u, pv = pidx ? p.vs_end[pc] : 0u;
   for (uint64_t e0 = 0; e0 < m; e0 += (uint64_t)G * EPP) {
     uint32_t klen[G], vlen[G], pos[G], np[G], kp[G];
     uint64_t ks[G], vs0[G];
     bool on[G];
+    const bool shuffled = e0 + (uint64_t)G * EPP < kWave;
 #pragma unroll
     for (uint32_t i = 0; i < G; i++) {
       const uint64_t r = e0 + i * EPP + lane / J;  // entry index inside the block
       on[i] = r < m;
       const uint64_t e = f + (on[i] ? r : m - 1);
-      ks[i] = key_start(p, e);
-      vs0[i] = vs_start(p, e);
-      const uint64_t kl64 = p.key_end[e] - ks[i], vl64 = p.vs_end[e] - vs0[i];
+      uint64_t ke, ve;
+      if (shuffled) {
+        const int rr = (int)(on[i] ? r : m - 1);
+        ks[i] = (uint32_t)__shfl((int)pk, rr);
+        ke = (uint32_t)__shfl((int)pk, rr + 1);
+        vs0[i] = (uint32_t)__shfl((int)pv, rr);
+        ve = (uint32_t)__shfl((int)pv, rr + 1);
+      } else {
+        ks[i] = key_start(p, e);
+        vs0[i] = vs_start(p, e);
+        ke = p.key_end[e];
+        ve = p.vs_end[e];
+      }
+      const uint64_t kl64 = ke - ks[i], vl64 = ve - vs0[i];
       klen[i] = (uint32_t)kl64;
       vlen[i] = (uint32_t)vl64;
       pos[i] = position(e, ks[i], vs0[i]);
