@@ -237,6 +237,20 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     HIPC(launch_decode_tile(p, c->stream));
     return LSMGPU_OK;
   }
+  if (path == 4) {  // fused stream-walk-scan-copy: blocks <= 4 KiB
+    const size_t meta_b = (size_t)nblk * kFscRec * 4;
+    if (meta_b > c->wsc.cap) {
+      HIPC(hipStreamSynchronize(c->stream));
+      HIPC(c->wsc.ensure(meta_b));
+    }
+    p.wmeta = c->wsc.as<uint32_t>();
+    p.wcap = kFscRec;
+    static const uint32_t ablate =
+        getenv("LSMGPU_ABLATE") ? (uint32_t)atoi(getenv("LSMGPU_ABLATE")) : 0u;
+    p.ablate = ablate;
+    HIPC(launch_decode_fsc(p, c->stream));
+    return LSMGPU_OK;
+  }
   if (path == 2) {  // walk-scan-copy: blocks of 4 KiB .. 64 KiB - 1
     // entries of a block (>= 10 B each) + the sentinel, rounded to 16-entry (128-B) chunks
     const uint32_t cap = (max_blk_len / 10 + 1 + 15) / 16 * 16;

@@ -323,7 +323,7 @@ def test_many_rounds(codec, oracle, monkeypatch, grid, shape):
     assert g.val_data.tobytes() == cols[2].tobytes()
 
 
-@pytest.mark.parametrize("path", ["wsc", "lds", "reg", "tile"])
+@pytest.mark.parametrize("path", ["wsc", "lds", "reg", "tile", "fsc"])
 def test_forced_decode_paths(codec, oracle, monkeypatch, path):
     """Every decode path (LSMGPU_DECODE_PATH: walk-scan-copy, LDS-lag, register-lag, fused tile) on the
     4 KiB block shapes: C2 4 KiB blocks, short entries, the KAT blocks (every
