@@ -275,6 +275,7 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local)
 
+    from lsmdb_amd import workload
     from lsmdb_amd.codec import Codec, MODE_MATERIALIZE, MODE_VIEW
     codec = Codec(local)
     stream = torch.cuda.Stream(device=dev)  # a real (non-null) stream shared with the events
@@ -331,8 +332,9 @@ def main():
         "dtype": "u8",
         "data": "synthetic (seeded; built on device by the gfx950 encoder)",
         "config": {
-            "workload": f"C{args.config}: {w['data_len']} B of SST data blocks per GPU, byte target "
-                        "4 KiB, 16 B keys / 100 B values, device-resident decode, materialize mode",
+            "workload": f"C{args.config}: {w['data_len']} B of SST data blocks per GPU, "
+                        f"{workload.DESCRIPTIONS[args.config]}, device-resident decode, "
+                        f"{'materialize' if mode & 1 else 'view'} mode",
             "blocks_per_gpu": w["nblocks"],
             "entries_per_gpu": w["n"],
             "max_block_bytes": w["max_len"],

@@ -229,7 +229,9 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
   p.glb = p.lb + nblk * 8;
   p.result = d_result;
   p.tag = c->tag;
-  const int path = decode_path(max_blk_len, (uint32_t)nblk);
+  int path = decode_path(max_blk_len, (uint32_t)nblk);
+  // the fused path DMAs whole 16-B lines: it needs a 16-B aligned buffer of >= 16 B
+  if (path == 4 && (((uintptr_t)d_data & 15) != 0 || data_len < 16)) path = 2;
   if (path == 3) {
     static const uint32_t ablate =
         getenv("LSMGPU_ABLATE") ? (uint32_t)atoi(getenv("LSMGPU_ABLATE")) : 0u;
@@ -248,7 +250,7 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     static const uint32_t ablate =
         getenv("LSMGPU_ABLATE") ? (uint32_t)atoi(getenv("LSMGPU_ABLATE")) : 0u;
     p.ablate = ablate;
-    HIPC(launch_decode_fsc(p, c->stream));
+    HIPC(launch_decode_fsc(p, c->num_cus, c->stream));
     return LSMGPU_OK;
   }
   if (path == 2) {  // walk-scan-copy: blocks of 4 KiB .. 64 KiB - 1

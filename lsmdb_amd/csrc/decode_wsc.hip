@@ -196,13 +196,15 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     if (tid == 255) s_first[256] = rel + n;
   }
   __syncthreads();
-  if (!p.view || (p.ablate & 2)) return;
+  if (!((p.mode & LSMGPU_MODE_VIEW) && p.view) || (p.ablate & 2)) return;  // mode 0: no view
   const uint32_t nt = s_first[256];
   const uint64_t e0 = s_ex[0];
   // entry -> block map in the walk's staging rows (free now): each thread marks its block's
   // entries, so the lookup is one LDS read (tiles of more entries: binary search)
   uint16_t* owner = reinterpret_cast<uint16_t*>(stage);
-  const bool mapped = nt <= 256 * kWalkStage * 4;  // u16 slots in the staging rows
+  // a u16 owner slot names one of the tile's 256 blocks
+  static_assert(256 <= 65536, "tile width must fit the u16 owner slot");
+  const bool mapped = nt <= (sizeof(stage) / (sizeof(uint16_t)));  // u16 slots in the staging rows
   if (mapped) {
     const uint32_t f = s_first[tid];
     for (uint32_t i = 0; i < n; i++) owner[f + i] = (uint16_t)tid;

@@ -152,11 +152,12 @@ hipError_t launch_encode(const EncodeParams& p, int num_cus, hipStream_t s);
 hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s);
 // fused tile decode (blocks <= 4 KiB): one launch, ticket-ordered tiles (p.gcnt[0] = 0)
 hipError_t launch_decode_tile(const DecodeParams& p, hipStream_t s);
-// fused stream-walk-scan-copy decode (blocks <= 4 KiB, decode_fsc.hip): one launch,
-// ticket-ordered 256-thread tiles (p.gcnt[0] = 0 between launches), per-block u32 entry
-// records in p.wmeta at stride p.wcap = kFscRec
+// fused persistent decode (blocks <= 4 KiB, decode_fsc.hip): one launch of <= num_cus
+// 512-thread workgroups (one per CU, all resident), chunk aggregates in p.lb (epoch-tagged),
+// per-block u32 entry records past the 64 kept in LDS in p.wmeta at stride p.wcap = kFscRec;
+// p.data 16-B aligned, p.data_len >= 16
 constexpr uint32_t kFscRec = 412;  // 409 entries of >= 10 B in 4096 B + the sentinel, rounded
-hipError_t launch_decode_fsc(const DecodeParams& p, hipStream_t s);
+hipError_t launch_decode_fsc(const DecodeParams& p, int num_cus, hipStream_t s);
 // which decode path a batch takes: 0 register-lag (<= 4 KiB), 1 LDS-lag, 2 walk-scan-copy
 // (blocks < 64 KiB, batches of >= kWscMinBlocks blocks), 3 fused tile (<= 4 KiB),
 // 4 fused stream-walk-scan-copy (<= 4 KiB)

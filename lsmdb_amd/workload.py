@@ -20,6 +20,14 @@ from dataclasses import dataclass
 import numpy as np
 
 SEED_BASE = 0x5EED0000
+# one-line workload labels per config (bench.py's config.workload)
+DESCRIPTIONS = {
+    1: "100 entries/block (reference resultInterval), 16 B keys / 100 B values",
+    2: "byte target 4 KiB, 16 B keys / 100 B values",
+    3: "byte target 4 KiB, 64 B keys / 1 KiB values",
+    4: "100 entries/block in 64 MiB SSTs, 16 B keys / 100 B values",
+    5: "byte target 32 KiB, Zipf(1.2) 8-256 B user keys + 8 B ts / 100 B values",
+}
 HEX = np.frombuffer(b"0123456789abcdef", dtype=np.uint8)
 META_A = 0x41          # 'A' as in table_test.go
 BIT_VALUE_POINTER = 2  # structs.go:33-40

@@ -123,12 +123,17 @@ def test_fsc_prefix_large_output(codec, oracle, fsc):
     _assert_same(codec.decode_host(data, off, ln), ref, "fsc prefix")
 
 
+@pytest.mark.parametrize("path", ["fsc", "wsc-fused-view", "wsc-copy"])
 @pytest.mark.parametrize("mode", ["view", "both", "none"])
-def test_fsc_modes_device(codec, oracle, fsc, mode):
-    """Device-resident calls in view-only, materialize+view and mode 0: view records match the
-    oracle; mode 0 leaves a passed view buffer untouched (advisor finding, round 1)."""
+def test_modes_device(codec, oracle, monkeypatch, path, mode):
+    """Device-resident calls in view-only, materialize+view and mode 0 on the fused path and on
+    walk-scan-copy (view epilogue in the walk forced on / off): view records match the oracle;
+    mode 0 leaves a passed view buffer untouched (advisor finding, round 1)."""
     import torch
     from lsmdb_amd.codec import MODE_MATERIALIZE, MODE_VIEW
+    monkeypatch.setenv("LSMGPU_DECODE_PATH", path[:3])
+    if path.startswith("wsc"):
+        monkeypatch.setenv("LSMGPU_WSC_VIEWFUSE", "1" if path == "wsc-fused-view" else "0")
     c, sst = _c2_sst(oracle, 60000, 21)
     sst = sst + b"{}" + (2).to_bytes(4, "big")
     off, ln, _, _ = oracle.parse_index(sst)

@@ -462,3 +462,38 @@ def test_wsc_many_tiles(codec, oracle):
     _assert_same(g, oracle.decode(sst, off, ln), "many tiles")
     assert g.key_data.tobytes() == c.keys.tobytes()
     assert g.val_data.tobytes() == c.vs.tobytes()
+
+
+@pytest.mark.parametrize("knob,val", [("LSMGPU_ENC_J", "4"), ("LSMGPU_ENC_J", "8"),
+                                      ("LSMGPU_ENC_J", "16"), ("LSMGPU_ENC_G", "2"),
+                                      ("LSMGPU_ENC_G", "4")])
+def test_encode_template_instances(codec, oracle, monkeypatch, knob, val):
+    """Every encode_kernel<J, G> instance the A/B knobs select (LSMGPU_ENC_J / LSMGPU_ENC_G)
+    changes which passes take the lane-shuffle offset path (advisor, round 1): each is checked
+    bit-exact against the oracle Builder on C1 / C2 / C5 and 100 / 180 entries per block."""
+    monkeypatch.setenv(knob, val)
+    for cfg, n, epb in [(1, 10000, None), (2, 20000, None), (5, 20000, None), (2, 20000, 100),
+                        (2, 20000, 180)]:
+        c = _cols(cfg, n, seed=n + 1)
+        e = c.entries_per_block if epb is None else epb
+        bb = c.block_bytes if epb is None else 0
+        ref, ref_dl, ref_rs = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, e, bb)
+        out, dl, rs = codec.encode_host(c.keys, c.key_end, c.vs, c.vs_end, e, bb)
+        assert dl == ref_dl and np.array_equal(rs, ref_rs)
+        assert out == ref, f"{knob}={val} cfg={cfg} epb={epb}"
+
+
+@pytest.mark.parametrize("lanes", ["8", "16"])
+def test_wsc_lanes_per_entry(codec, oracle, monkeypatch, lanes):
+    """Walk-scan-copy with 8 or 16 lanes per entry forced (LSMGPU_WSC_J): the copy's
+    preloaded-record shuffle path runs on different passes for each (advisor, round 1)."""
+    monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
+    monkeypatch.setenv("LSMGPU_WSC_J", lanes)
+    c5 = _cols(5, 30000, seed=19)
+    c2 = _cols(2, 30000, seed=20)
+    parts = [oracle.build_cols(c5.keys, c5.key_end, c5.vs, c5.vs_end, c5.entries_per_block,
+                               c5.block_bytes)[0],
+             oracle.build_cols(c2.keys, c2.key_end, c2.vs, c2.vs_end, 0, 4096)[0],
+             oracle.build_cols(*_random_cols(30000, 4), 0, 4096)[0]]
+    data, off, ln = _sst_blocks(oracle, parts)
+    _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln), f"J={lanes}")
