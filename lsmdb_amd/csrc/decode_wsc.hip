@@ -62,21 +62,102 @@ __device__ __forceinline__ void flush_meta(uint2* dst, const uint2* row, uint32_
   }
 }
 
+// ---- streaming walk (blocks <= 4 KiB): the tile's blocks pass through LDS kSwSub at a time
+constexpr uint32_t kSwSub = 8;       // blocks per LDS sub-batch
+constexpr uint32_t kSwSlot = 4128;   // a <= 4096-B block at any 16-B shift + the 8-B header
+                                     // over-read, as 258 16-B chunks
+constexpr uint32_t kSwMaxLen = 4096;
+constexpr uint32_t kSwTile = 256;    // blocks per streaming-walk tile (64-block tiles: slower)
+
+__device__ __forceinline__ uint4 sw_chunk(const DecodeParams& p, uint32_t off, uint32_t len,
+                                          uint32_t c) {
+  // chunk c of block [off, off + len)'s 16-B aligned span; zero past it or past the data
+  if (len > kSwMaxLen || (uint64_t)off + len > p.data_len) return make_uint4(0, 0, 0, 0);
+  const uint32_t a0 = off & ~15u;
+  if (c >= (((off - a0) + len + 15) >> 4)) return make_uint4(0, 0, 0, 0);
+  const uint64_t a = (uint64_t)a0 + 16ull * c;
+  if (a + 16 <= p.data_len) return *reinterpret_cast<const uint4*>(p.data + a);
+  uint4 v = make_uint4(0, 0, 0, 0);  // the line crossing the end of the data buffer
+  for (int i = 0; i < 16; i++)
+    if (a + i < p.data_len) set_byte(v, i, p.data[a + i]);
+  return v;
+}
+
+// One block's walk (blockIterator.Next/parseKV, table/iterator.go:93-135) over `src` (LDS slot
+// or global bytes), writing the metadata records {header pos | value offset << 16, key offset}
+// + the sentinel straight to `meta`.  A fast loop takes plen == 0 entries (all Builder writes,
+// SURVEY F1) with one 8-B header read each; the general loop continues from wherever it stops
+// and applies every stop rule in the iterator's order.
+template <class Src>
+__device__ __forceinline__ WalkResult walk_meta(const Src& src, const uint8_t* fast, uint32_t len,
+                                                uint2* meta) {
+  uint32_t pos = 0, n = 0, K = 0, V = 0, st = LSMGPU_BLK_OK;
+  if (fast) {
+    for (;;) {
+      uint2 hw;
+      __builtin_memcpy(&hw, fast + pos, 8);  // pos <= len keeps the read inside the block's span
+      const uint32_t plen = __builtin_amdgcn_perm(0u, hw.x, 0x0c0c0001u);
+      const uint32_t klen = __builtin_amdgcn_perm(0u, hw.x, 0x0c0c0203u);
+      const uint32_t vlen = __builtin_amdgcn_perm(0u, hw.y, 0x0c0c0001u);
+      const uint32_t end = pos + 10 + klen + vlen;
+      if ((len - pos < 10) | (klen == 0) | (plen != 0) | (end > len)) break;
+      meta[n] = make_uint2(pos | (V << 16), K);
+      K += klen;
+      V += vlen;
+      n++;
+      pos = end;
+    }
+  }
+  for (;;) {
+    if (pos >= len) break;                                   // iterator.go:115-118
+    if (len - pos < 10) { st = LSMGPU_BLK_TRUNC_HEADER; break; }
+    const Hdr h = src.hdr(pos);                              // iterator.go:121
+    if ((h.klen | h.plen) == 0) break;                       // iterator.go:124-127
+    if (n == 0 && h.plen != 0) { st = LSMGPU_BLK_FIRST_PLEN; break; }  // iterator.go:129-133
+    if (10 + h.plen > len) { st = LSMGPU_BLK_PREFIX_OOB; break; }      // base key = entry 0's
+    const uint32_t end = pos + 10 + h.klen + h.vlen;         // iterator.go:101-109
+    if (end > len) { st = LSMGPU_BLK_VALUE_OVERFLOW; break; }
+    meta[n] = make_uint2(pos | (V << 16), K);
+    K += h.plen + h.klen;
+    V += h.vlen;
+    n++;
+    pos = end;
+  }
+  meta[n] = make_uint2(pos | (V << 16), K);  // sentinel
+  return WalkResult{n, K, V, st};
+}
+
 // K1: lane = block; a workgroup = a tile of 256 consecutive blocks, tiles taken in ticket order
 // (p.gcnt[0]).  After the walk the workgroup scans its blocks' {entries, key bytes, value
 // bytes}, publishes the tile aggregate and finds the tile's output base by decoupled look-back
 // over the tile records (epoch-tagged granules in p.lb), then writes every block's exclusive
 // base: the output bases are known when the walk ends, with no separate scan launch.  The
 // ticket makes every predecessor tile already running, so the look-back always progresses.
+// STREAM = false: lane b walks block b straight from HBM, one dependent 8-B header load per
+// entry (every 128-B line of the input is fetched on its own, as scattered requests).
+// STREAM = true (p.wstream, blocks <= 4 KiB): the tile's blocks go through LDS kSwSub at a time,
+// every thread loading one 16-B chunk of each block of the NEXT sub-batch (coalesced, 1 KiB per
+// wave instruction) while wave 0 walks the current one from LDS, one lane per block.  An LDS
+// walk costs ~210 cycles per entry in latency whatever the number of lanes walking
+// (scripts/walk_probe.hip), so it pays when many blocks walk at once and nothing else holds the
+// bytes in LDS -- as here, where the copy is a separate launch.
+template <bool STREAM, uint32_t TB>  // TB = blocks per tile (<= 256 threads: thread t owns block t)
 __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
-  __shared__ uint2 stage[256 * kWalkStage];
+  static_assert(TB <= 256, "one thread per block of the tile");
+  constexpr uint32_t kStageBytes = 256 * kWalkStage * sizeof(uint2);
+  constexpr uint32_t kLdsBytes = STREAM ? kSwSub * kSwSlot : kStageBytes;
+  static_assert(STREAM || kLdsBytes == kStageBytes, "the HBM walk stages 16 records per lane");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+  uint2* const stage = reinterpret_cast<uint2*>(lds);
   __shared__ uint32_t s_tile;
   __shared__ uint32_t s_wave[4][3];
   __shared__ uint32_t s_ex[3];
   __shared__ uint32_t s_first[257];  // p.wfuse: tile-relative first entry of each block
-  __shared__ uint32_t s_off[256];    // p.wfuse: each block's input offset
+  __shared__ uint32_t s_off[256];    // each block's input offset
+  __shared__ uint32_t s_len[STREAM ? 256 : 1];
+  __shared__ uint32_t s_res[STREAM ? 4 : 1][STREAM ? 256 : 1];  // stream walk: n, K, V, status
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-  const uint32_t ntiles = (p.nblk + 255) / 256;
+  const uint32_t ntiles = (p.nblk + TB - 1) / TB;
   if (tid == 0) {
     const uint32_t t = atomicAdd(p.gcnt, 1u);
     if (t == ntiles - 1) atomicExch(p.gcnt, 0u);  // every ticket is taken
@@ -84,9 +165,75 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   }
   __syncthreads();
   const uint32_t tile = s_tile;
-  const uint32_t b = tile * 256 + tid;
+  // thread t owns block tile * TB + t (threads past TB own none: zero entries)
+  const uint32_t b = tid < TB ? tile * TB + tid : 0xffffffffu;
   uint32_t n = 0, K = 0, V = 0, st = LSMGPU_BLK_OK;
-  if (b < p.nblk) {
+  if constexpr (STREAM) {
+    const uint32_t nb = min(TB, p.nblk - tile * TB);
+    const uint32_t nsub = (nb + kSwSub - 1) / kSwSub;
+    if (b < p.nblk) {
+      s_off[tid] = p.blk_off[b];
+      s_len[tid] = p.blk_len[b];
+    }
+    __syncthreads();
+    uint4 R[kSwSub], RT;
+    auto issue = [&](uint32_t j) {
+#pragma unroll
+      for (uint32_t i = 0; i < kSwSub; i++) {
+        const uint32_t bi = j * kSwSub + i;
+        R[i] = bi < nb ? sw_chunk(p, s_off[bi], s_len[bi], tid) : make_uint4(0, 0, 0, 0);
+      }
+      const uint32_t ti = j * kSwSub + (tid >> 1);  // chunks 256, 257 of each block
+      RT = (tid < 2 * kSwSub && ti < nb) ? sw_chunk(p, s_off[ti], s_len[ti], 256 + (tid & 1))
+                                         : make_uint4(0, 0, 0, 0);
+    };
+    issue(0);
+    for (uint32_t j = 0; j < nsub; j++) {
+      __syncthreads();  // the previous sub-batch's walk is done with the buffer
+#pragma unroll
+      for (uint32_t i = 0; i < kSwSub; i++)
+        *reinterpret_cast<uint4*>(lds + i * kSwSlot + 16 * tid) = R[i];
+      if (tid < 2 * kSwSub)
+        *reinterpret_cast<uint4*>(lds + (tid >> 1) * kSwSlot + 16 * (256 + (tid & 1))) = RT;
+      __syncthreads();
+      if (j + 1 < nsub) issue(j + 1);  // in flight while wave 0 walks sub-batch j
+      const uint32_t bi = j * kSwSub + lane;
+      if (wave == 0 && lane < kSwSub && bi < nb) {
+        const uint32_t off = s_off[bi], len = s_len[bi];
+        uint2* meta = reinterpret_cast<uint2*>(p.wmeta) + (uint64_t)(tile * TB + bi) * p.wcap;
+        WalkResult r{0, 0, 0, LSMGPU_BLK_RANGE};
+        if ((uint64_t)off + len > p.data_len) {
+          meta[0] = make_uint2(0, 0);
+        } else if (p.ablate & 4) {  // timing only: no walk
+          r = WalkResult{0, 0, 0, LSMGPU_BLK_OK};
+          meta[0] = make_uint2(0, 0);
+        } else if (len > kSwMaxLen) {  // only if the caller's max_blk_len was wrong: global walk
+          r = walk_meta(GlobalSrc{p.data + off}, nullptr, len, meta);
+        } else {
+          const uint8_t* slot = lds + lane * kSwSlot;
+          r = walk_meta(LdsSrc{slot, off & 15u}, slot + (off & 15u), len, meta);
+        }
+        s_res[0][bi] = r.n;
+        s_res[1][bi] = r.K;
+        s_res[2][bi] = r.V;
+        s_res[3][bi] = r.status;
+      }
+    }
+    // the records are global stores of wave 0: complete before other waves read them
+    if (wave == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (b < p.nblk) {
+      n = s_res[0][tid];
+      K = s_res[1][tid];
+      V = s_res[2][tid];
+      st = s_res[3][tid];
+      uint64_t* t = p.wstat + 3ull * b;
+      t[0] = n;
+      t[1] = K;
+      t[2] = V;
+      p.wstatus[b] = st;
+    }
+  } else if (b < p.nblk) {
     uint2* row = stage + tid * kWalkStage;
     const uint32_t off = p.blk_off[b], len = p.blk_len[b];
     uint32_t pos = 0;
@@ -204,7 +351,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   uint16_t* owner = reinterpret_cast<uint16_t*>(stage);
   // a u16 owner slot names one of the tile's 256 blocks
   static_assert(256 <= 65536, "tile width must fit the u16 owner slot");
-  const bool mapped = nt <= (sizeof(stage) / (sizeof(uint16_t)));  // u16 slots in the staging rows
+  const bool mapped = nt <= kLdsBytes / sizeof(uint16_t);  // u16 slots in the walk's LDS
   if (mapped) {
     const uint32_t f = s_first[tid];
     for (uint32_t i = 0; i < n; i++) owner[f + i] = (uint16_t)tid;
@@ -223,7 +370,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     const uint64_t bend = e0 + s_first[lo + 1];
     if (bend > p.ent_cap || bend > 0xffffffffull) continue;  // reported above (result[5])
     const uint32_t i = e - s_first[lo];
-    const uint2* meta = reinterpret_cast<const uint2*>(p.wmeta) + (uint64_t)(tile * 256 + lo) * p.wcap;
+    const uint2* meta = reinterpret_cast<const uint2*>(p.wmeta) + (uint64_t)(tile * TB + lo) * p.wcap;
     const uint2 m0 = meta[i], m1 = meta[i + 1];
     const uint32_t hp = m0.x & 0xffffu, vl = (m1.x >> 16) - (m0.x >> 16);
     const uint32_t kl = (m1.x & 0xffffu) - hp - 10 - vl;  // stored key bytes
@@ -672,7 +819,11 @@ hipError_t launch_decode_tile(const DecodeParams& p, hipStream_t s) {
 
 hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s) {
   const uint32_t nblk = p.nblk;
-  hipLaunchKernelGGL(wsc_walk_kernel, dim3((nblk + 255) / 256), dim3(256), 0, s, p);
+  if (p.wstream)
+    hipLaunchKernelGGL((wsc_walk_kernel<true, kSwTile>), dim3((nblk + kSwTile - 1) / kSwTile),
+                       dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((wsc_walk_kernel<false, 256>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || p.wfuse) return e;  // view-only: the walk wrote everything
   const uint32_t per_wg = 4 / p.wsplit;  // blocks per 4-wave workgroup

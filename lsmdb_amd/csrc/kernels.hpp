@@ -46,6 +46,7 @@ struct DecodeParams {
   uint32_t wj;              // walk-scan-copy: lanes per entry forced (8, 16), 0 = per block
   uint32_t wfuse;           // walk-scan-copy, view-only mode: the walk writes the view index
                             // and per-block outputs itself (no copy launch)
+  uint32_t wstream;         // walk-scan-copy: blocks <= 4 KiB streamed through LDS for the walk
 };
 
 // Encode: one wave per output block; every byte position is closed-form

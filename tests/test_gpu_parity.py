@@ -497,3 +497,48 @@ def test_wsc_lanes_per_entry(codec, oracle, monkeypatch, lanes):
              oracle.build_cols(*_random_cols(30000, 4), 0, 4096)[0]]
     data, off, ln = _sst_blocks(oracle, parts)
     _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln), f"J={lanes}")
+
+
+@pytest.mark.parametrize("walk", ["stream", "global"])
+@pytest.mark.parametrize("mode", ["materialize", "view"])
+def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
+    """Walk-scan-copy's two walks (LSMGPU_WSC_WALK): blocks <= 4 KiB streamed through LDS 16 at a
+    time (the default) or walked lane by lane from HBM.  C2 / C3 blocks, short and tiny entries
+    (> 64 per block), every KAT block (error statuses, terminators, plen > 0) at odd alignments,
+    prefix-compressed random blocks, a ragged last tile and a block ending at the buffer's end."""
+    from lsmdb_amd.codec import MODE_MATERIALIZE, MODE_VIEW
+    monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
+    monkeypatch.setenv("LSMGPU_WSC_WALK", walk)
+    monkeypatch.setenv("LSMGPU_WSC_VIEWFUSE", "1")
+    c2 = _cols(2, 40000, seed=23)
+    c3 = _cols(3, 3000, seed=24)
+    parts = [oracle.build_cols(c2.keys, c2.key_end, c2.vs, c2.vs_end, 0, 4096)[0],
+             oracle.build_cols(c3.keys, c3.key_end, c3.vs, c3.vs_end, 0, 4096)[0],
+             oracle.build_cols(*_random_cols(20000, 25), 0, 4096)[0],
+             oracle.build_cols(*_random_cols(60000, 26, 9, 10, 3, 4), 0, 4096)[0]]
+    data, off, ln = _sst_blocks(oracle, parts)
+    kd = bytearray(data)
+    offs, lens = list(off), list(ln)
+    for i, (_n, block, _e, _s) in enumerate(K.DECODE_KATS * 3):
+        kd += b"\xab" * (i % 13)
+        offs.append(len(kd))
+        lens.append(len(block))
+        kd += block
+    kd = bytes(kd)
+    o2, l2 = np.array(offs, np.uint32), np.array(lens, np.uint32)
+    m = MODE_MATERIALIZE | MODE_VIEW if mode == "materialize" else MODE_VIEW
+    for sl in (slice(None), slice(len(off) - 700, None), slice(None, None, -1)):
+        oo, ll = np.ascontiguousarray(o2[sl]), np.ascontiguousarray(l2[sl])
+        g = codec.decode_host(kd, oo, ll, mode=m)
+        o = oracle.decode(kd, oo, ll)
+        if mode == "materialize":
+            _assert_same(g, o, f"{walk} {sl}")
+        else:
+            assert g.n_entries == o.n_entries and np.array_equal(g.view, o.view)
+            assert np.array_equal(g.blk_first, o.blk_first)
+            assert np.array_equal(g.blk_status, o.blk_status)
+    # the last block ends exactly at the end of the buffer (the streamed line crossing it)
+    sst = parts[0]
+    so, sl_, _, _ = oracle.parse_index(sst + b"{}" + (2).to_bytes(4, "big"))
+    tight = sst[: int(so[-1]) + int(sl_[-1])]
+    _assert_same(codec.decode_host(tight, so, sl_), oracle.decode(tight, so, sl_), "tight end")
