@@ -148,19 +148,24 @@ __device__ __forceinline__ void copy_block_lds(const DecodeParams& p, const uint
         uint8_t* d[G];
 #pragma unroll
         for (int i = 0; i < G; i++) {
-          d[i] = nullptr;
-          if (q < np[i]) {
-            const bool key = q < kp[i];
-            const uint32_t len = key ? kl[i] : vl[i];
-            const uint32_t o = min(16 * (key ? q : q - kp[i]), len - 16);
-            const uint32_t x = sh + hp[i] + 10 + (key ? 0u : kl[i]) + o;
-            __builtin_memcpy(&v[i], slot + x, 16);
-            d[i] = (key ? kbase + ko[i] : vbase + vo[i]) + o;
-          }
+          // every lane reads (an inactive piece reads slot byte 0): v[i] is defined on every
+          // path, so it stays in registers
+          const bool act = q < np[i];
+          const bool key = q < kp[i];
+          const uint32_t len = key ? kl[i] : vl[i];
+          const uint32_t o = min(16 * (key ? q : q - kp[i]), len - 16);
+          const uint32_t x = act ? sh + hp[i] + 10 + (key ? 0u : kl[i]) + o : 0u;
+          // a typed (misaligned) ds_read_b128: taking v[i]'s address for memcpy would keep
+          // the array in scratch
+          v[i] = *reinterpret_cast<const uint4*>(slot + x);
+          d[i] = act ? (key ? kbase + ko[i] : vbase + vo[i]) + o : nullptr;
         }
 #pragma unroll
         for (int i = 0; i < G; i++)
-          if (d[i]) __builtin_memcpy(d[i], &v[i], 16);
+          if (d[i]) {
+            const uint4 t = v[i];
+            __builtin_memcpy(d[i], &t, 16);
+          }
       }
       continue;
     }
@@ -552,6 +557,258 @@ __global__ void __launch_bounds__(512) fsc_kernel(DecodeParams p) {
   if (p.stamps && tid == 0) atomicAdd(reinterpret_cast<unsigned long long*>(p.stamps + 12), (unsigned long long)R);
 }
 
+// ============================================================ wave-owned blocks (default)
+// A 512-thread workgroup takes the next tile of 16 consecutive blocks from an ordered ticket
+// (p.gcnt[0]); each wave OWNS two of them for the workgroup's whole life:
+//   load   : both blocks' 16-B aligned spans into registers (coalesced, 1 KiB per instruction),
+//            then into the wave's two LDS slots;
+//   walk   : lanes 0 and 1 walk the two blocks from LDS (blockIterator.Next/parseKV,
+//            table/iterator.go:93-135), records {header pos | stored key bytes << 16} to the LDS
+//            pool (entries 0..63; later ones to global scratch);
+//   scan   : after a barrier wave 0 scans the 16 blocks, publishes the tile aggregate and finds
+//            the tile's output base by decoupled look-back over the earlier tiles' records (the
+//            ticket makes every earlier tile already running, so it always progresses);
+//   copy   : after a barrier every wave copies its two blocks out of LDS (8 lanes per entry,
+//            16-B pieces, unaligned global stores) + key_end / val_end / view records.
+// An LDS walk is latency-bound (~210 cycles per entry whatever the number of lanes walking,
+// scripts/walk_probe.hip), so what sets its throughput is how many blocks walk at once: here
+// every resident block does -- 32 per CU at two workgroups per CU -- against 12-16 in the
+// slot-ring designs, where only one slot of the ring is being walked.
+constexpr uint32_t kWbWaves = 8;  // waves per workgroup (4: 0.90 vs 0.86 ms, C2 1 GiB)
+constexpr uint32_t kWbPer = 2;    // blocks per wave
+constexpr uint32_t kWbTile = kWbWaves * kWbPer;  // blocks per tile
+
+__device__ __forceinline__ void walk_block_lds(const DecodeParams& p, const uint8_t* slot,
+                                               uint32_t off, uint32_t len, uint32_t* pr,
+                                               uint32_t* gr, uint32_t& n_, uint32_t& K_,
+                                               uint32_t& V_, uint32_t& st_, bool& any_plen) {
+  uint32_t n = 0, K = 0, V = 0, S = 0, pos = 0, st = LSMGPU_BLK_OK;
+  if (!blk_fits(p, off, len)) {
+    st = LSMGPU_BLK_RANGE;
+  } else {
+    const uint8_t* const sb = slot + (off & 15u);
+    // fast loop: plen == 0 entries (every entry Builder writes) while the records
+    // fit the LDS pool; anything else leaves the rest of the block to the general loop
+    for (;;) {
+      uint2 hw;
+      __builtin_memcpy(&hw, sb + pos, 8);  // pos <= len keeps the read inside the slot
+      const uint32_t plen = __builtin_amdgcn_perm(0u, hw.x, 0x0c0c0001u);
+      const uint32_t klen = __builtin_amdgcn_perm(0u, hw.x, 0x0c0c0203u);
+      const uint32_t vlen = __builtin_amdgcn_perm(0u, hw.y, 0x0c0c0001u);
+      const uint32_t end = pos + 10 + klen + vlen;
+      if ((len - pos < 10) | (klen == 0) | (plen != 0) | (end > len) | (n >= kPoolRec - 1)) break;
+      pr[n] = pos | (S << 16);
+      S += klen;
+      n++;
+      pos = end;
+    }
+    K = S;
+    V = pos - 10 * n - S;
+    // general loop: prefix-compressed entries and every stop rule, in the iterator's order
+    const LdsSrc src{slot, off & 15u};
+    for (;;) {
+      const Hdr h = src.hdr(pos);
+      const uint32_t end = pos + 10 + h.klen + h.vlen;
+      const bool eof = pos >= len;                              // iterator.go:115-118
+      const bool trunc = len - pos < 10;
+      const bool term = (h.klen | h.plen) == 0;                 // iterator.go:124-127
+      const bool fplen = n == 0 && h.plen != 0;                 // iterator.go:129-133
+      const bool poob = 10 + h.plen > len;                      // base key = entry 0's
+      const bool vovf = end > len;                              // iterator.go:101-106
+      if (eof | trunc | term | fplen | poob | vovf) {
+        st = (eof | (!trunc & term)) ? LSMGPU_BLK_OK
+             : trunc                 ? LSMGPU_BLK_TRUNC_HEADER
+             : fplen                 ? LSMGPU_BLK_FIRST_PLEN
+             : poob                  ? LSMGPU_BLK_PREFIX_OOB
+                                     : LSMGPU_BLK_VALUE_OVERFLOW;
+        break;
+      }
+      const uint32_t rec = pos | (S << 16);
+      if (n < kPoolRec) pr[n] = rec;
+      else gr[n] = rec;
+      any_plen = any_plen || h.plen != 0;
+      K += h.plen + h.klen;
+      S += h.klen;
+      V += h.vlen;
+      n++;
+      pos = end;
+    }
+  }
+  const uint32_t rec = pos | (S << 16);  // sentinel
+  if (n < kPoolRec) pr[n] = rec;
+  else gr[n] = rec;
+  n_ = n;
+  K_ = K;
+  V_ = V;
+  st_ = st;
+}
+
+__global__ void __launch_bounds__(kWbWaves * 64) fsw_kernel(DecodeParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t slots[kWbTile * kFscSlot];
+  __shared__ uint32_t pool[kWbTile * kPoolRec];
+  __shared__ uint32_t s_n[kWbTile], s_k[kWbTile], s_v[kWbTile], s_st[kWbTile], s_off[kWbTile];
+  __shared__ uint32_t s_bn[kWbTile], s_bk[kWbTile], s_bv[kWbTile];
+  __shared__ uint32_t s_slow, s_ok, s_tile;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint32_t nblk = p.nblk;
+  uint64_t t_prev = p.stamps ? __builtin_amdgcn_s_memtime() : 0;
+#define FSW_STAMP(i)                                                                       \
+  if (p.stamps && lane == 0 && wave <= 1) {                                                \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();                                      \
+    atomicAdd(reinterpret_cast<unsigned long long*>(p.stamps + (i) + 8 * wave), t_ - t_prev); \
+    t_prev = t_;                                                                           \
+  }
+  const uint32_t ntiles = (nblk + kWbTile - 1) / kWbTile;
+  if (tid == 0) {
+    const uint32_t t = atomicAdd(p.gcnt, 1u);
+    if (t == ntiles - 1) atomicExch(p.gcnt, 0u);  // every ticket is taken
+    s_tile = t;
+    s_slow = 0;
+  }
+  __syncthreads();
+  FSW_STAMP(0)  // ticket
+  const uint32_t tile = s_tile;
+  const uint32_t b0 = tile * kWbTile;
+  const uint32_t nb = min(kWbTile, nblk - b0);
+  uint32_t* const wm = p.wmeta;
+
+  // ---- load: the wave's two blocks, registers -> its LDS slots
+  const uint32_t wb = kWbPer * wave;  // the wave's first block in the tile
+  uint32_t o = 0, l = 0xffffffffu;
+  if (lane < kWbPer && wb + lane < nb) {
+    o = p.blk_off[b0 + wb + lane];
+    l = p.blk_len[b0 + wb + lane];
+  }
+  {
+    const uint64_t last = p.data_len >= 16 ? ((p.data_len - 16) & ~15ull) : 0ull;
+    uint4 v[kWbPer][5];
+#pragma unroll
+    for (uint32_t x = 0; x < kWbPer; x++) {
+      const uint32_t off = readlane(o, x), len = readlane(l, x);
+      const uint64_t a0 = blk_fits(p, off, len) ? (uint64_t)(off & ~15u) : 0ull;
+#pragma unroll
+      for (uint32_t q = 0; q < 5; q++) {  // unconditional, clamped: no register merge, no wait
+        uint64_t a = a0 + 16ull * (lane + q * kWave);
+        a = a < last ? a : last;
+        v[x][q] = *reinterpret_cast<const uint4*>(p.data + a);
+      }
+    }
+    FSW_STAMP(1)  // [off, len) + load issue
+#pragma unroll
+    for (uint32_t x = 0; x < kWbPer; x++) {
+      uint8_t* dst = slots + (wb + x) * kFscSlot;
+#pragma unroll
+      for (uint32_t q = 0; q < 5; q++) {
+        const uint32_t c = lane + q * kWave;
+        if (c < kFscChunks) *reinterpret_cast<uint4*>(dst + 16 * c) = v[x][q];
+      }
+      fix_tail(p, dst, readlane(o, x), readlane(l, x), lane);
+    }
+  }
+  FSW_STAMP(2)  // load wait + LDS writes
+  // ---- walk: lanes 0, 1 (a wave's LDS operations complete in order: no fence needed)
+  {
+    const uint32_t bi = wb + lane;
+    const bool has = lane < kWbPer && bi < nb;
+    bool any_plen = false;
+    if (has) {
+      uint32_t n, K, V, st;
+      walk_block_lds(p, slots + bi * kFscSlot, o, l, pool + bi * kPoolRec,
+                     wm + (uint64_t)(b0 + bi) * p.wcap, n, K, V, st, any_plen);
+      s_n[bi] = n;
+      s_k[bi] = K;
+      s_v[bi] = V;
+      s_st[bi] = st;
+      s_off[bi] = o;
+    }
+    const uint64_t sm = __ballot(has && any_plen);
+    if (lane == 0 && sm) atomicOr(&s_slow, (uint32_t)sm << wb);
+  }
+  FSW_STAMP(3)  // walk
+  // records past 63 went to global scratch: complete them before other waves may read them
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  FSW_STAMP(4)  // barrier (the slowest walk)
+
+  // ---- scan + look-back + per-block outputs (wave 0: lane = block)
+  if (wave == 0) {
+    const bool has = lane < nb;
+    const uint32_t n = has ? s_n[lane] : 0u, K = has ? s_k[lane] : 0u, V = has ? s_v[lane] : 0u;
+    const uint32_t in_ = wave_scan_sat(n, lane), ik = wave_scan_sat(K, lane),
+                   iv = wave_scan_sat(V, lane);
+    const uint32_t tn = readlane(in_, 63), tk = readlane(ik, 63), tv = readlane(iv, 63);
+    uint64_t* Rr = p.lb + (uint64_t)tile * 8;
+    Tot ex{0, 0, 0};
+    if (tile > 0) {
+      store3(Rr, p.tag, tn, tk, tv, lane);
+      ex = lookback(p.lb, tile, p.tag, lane, p.result);
+    }
+    store3(Rr + 4, p.tag, sat_add(ex.n, tn), sat_add(ex.k, tk), sat_add(ex.v, tv), lane);
+    bool ok = false;
+    if (has) {
+      const uint32_t b = b0 + lane, st = s_st[lane];
+      const uint32_t en = sat_add(ex.n, in_ - n),
+                     ek = sat_add(ex.k, ik == 0xffffffffu ? ik : ik - K),
+                     ev = sat_add(ex.v, iv - V);
+      s_bn[lane] = en;
+      s_bk[lane] = ek;
+      s_bv[lane] = ev;
+      ok = (uint64_t)en + n <= p.ent_cap && (uint64_t)en + n <= 0xffffffffull;
+      if (p.mode & LSMGPU_MODE_MATERIALIZE) {
+        const uint64_t kend = (uint64_t)ek + K, vend = (uint64_t)ev + V;
+        ok = ok && (kend <= p.key_cap || !p.key_data) && (vend <= p.val_cap || !p.val_data);
+        ok = ok && kend < 0xffffffffull && vend <= 0xffffffffull;
+      }
+      if (p.blk_first) p.blk_first[b] = en;
+      if (p.blk_status) p.blk_status[b] = (int32_t)st;
+      if (st != LSMGPU_BLK_OK) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(p.result + 4), 1ull);
+        atomicMax(reinterpret_cast<unsigned long long*>(p.result + 3),
+                  (unsigned long long)(nblk - b));
+      }
+      if (b == nblk - 1) {  // totals of the whole batch
+        if (p.blk_first) p.blk_first[nblk] = (uint32_t)((uint64_t)en + n);
+        p.result[0] = (uint64_t)en + n;
+        p.result[1] = (uint64_t)ek + K;
+        p.result[2] = (uint64_t)ev + V;
+      }
+      if (!ok) atomicOr(reinterpret_cast<unsigned long long*>(p.result + 5), 1ull);
+    }
+    const uint64_t okm = __ballot(ok);
+    if (lane == 0) s_ok = (uint32_t)okm;
+  }
+  __syncthreads();
+  FSW_STAMP(5)  // scan + look-back + outputs
+  if (p.ablate & 2) return;
+
+  // ---- copy: each wave its two blocks, out of LDS
+  const bool mat = (p.mode & LSMGPU_MODE_MATERIALIZE) != 0;
+  const bool view = (p.mode & LSMGPU_MODE_VIEW) != 0 && p.view;
+  if (!mat && !view) return;
+  const uint32_t okm = s_ok, slowm = s_slow;
+#pragma unroll
+  for (uint32_t x = 0; x < kWbPer; x++) {
+    const uint32_t bi = wb + x;
+    if (bi >= nb) break;
+    const uint32_t n = uniform(s_n[bi]);
+    if (n == 0 || !((okm >> bi) & 1)) continue;
+    const uint64_t en = uniform(s_bn[bi]), ek = uniform(s_bk[bi]), ev = uniform(s_bv[bi]);
+    const uint32_t off = uniform(s_off[bi]);
+    if ((slowm >> bi) & 1) {
+      copy_block_slow(p, p.data + off, n, en, ek, ev, off, mat, view, lane);
+      continue;
+    }
+    uint8_t* kbase = (mat && p.key_data) ? p.key_data + ek : nullptr;
+    uint8_t* vbase = (mat && p.val_data) ? p.val_data + ev : nullptr;
+    copy_block_lds<8, 5>(p, pool + bi * kPoolRec, wm + (uint64_t)(b0 + bi) * p.wcap,
+                         slots + bi * kFscSlot, off & 15u, kbase, vbase, n, en, ek, ev, off, mat,
+                         view, lane);
+  }
+  FSW_STAMP(6)  // copy
+  if (p.stamps && tid == 0) atomicAdd(reinterpret_cast<unsigned long long*>(p.stamps + 7), 1ull);
+#undef FSW_STAMP
+}
+
 hipError_t launch_decode_fsc(const DecodeParams& p, int num_cus, hipStream_t s) {
   const uint32_t nchunks = (p.nblk + kChunk - 1) / kChunk;
   uint32_t G = (uint32_t)(num_cus < (int)kMaxGrid ? num_cus : (int)kMaxGrid);
@@ -566,6 +823,24 @@ hipError_t launch_decode_fsc(const DecodeParams& p, int num_cus, hipStream_t s) 
       (void)hipMemsetAsync(stamps, 0, 16 * sizeof(uint64_t), s);
       q.stamps = stamps;
     }
+  }
+  // LSMGPU_FSC=ring: the persistent slot-ring kernel; default: wave-owned blocks
+  static const bool ring = getenv("LSMGPU_FSC") && getenv("LSMGPU_FSC")[0] == 'r';
+  if (!ring) {
+    hipLaunchKernelGGL(fsw_kernel, dim3((p.nblk + kWbTile - 1) / kWbTile), dim3(kWbWaves * 64), 0, s, q);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && q.stamps) {
+      uint64_t h[16] = {0};
+      (void)hipMemcpyAsync(h, stamps, sizeof(h), hipMemcpyDeviceToHost, s);
+      (void)hipStreamSynchronize(s);
+      const double t = h[7] ? (double)h[7] : 1.0;
+      fprintf(stderr, "[lsmgpu] fsw stamps per tile (cycles) wave0|wave1: ticket %.0f|%.0f "
+              "issue %.0f|%.0f loadwait %.0f|%.0f walk %.0f|%.0f barrier %.0f|%.0f scan %.0f|%.0f "
+              "copy %.0f|%.0f | tiles %llu\n", h[0] / t, h[8] / t, h[1] / t, h[9] / t, h[2] / t,
+              h[10] / t, h[3] / t, h[11] / t, h[4] / t, h[12] / t, h[5] / t, h[13] / t, h[6] / t,
+              h[14] / t, (unsigned long long)h[7]);
+    }
+    return e;
   }
   hipLaunchKernelGGL(fsc_kernel, dim3(G), dim3(512), 0, s, q);
   hipError_t e = hipGetLastError();
