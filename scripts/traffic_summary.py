@@ -18,7 +18,7 @@ import os
 import sys
 
 PIPELINE = ("lsmgpu::decode", "wsc_walk_kernel", "wsc_copy_kernel", "wsc_carry_kernel", "Tri64",
-            "tile_decode_kernel")
+            "tile_decode_kernel", "fsw_kernel", "fsc_kernel")
 
 
 def per_launch(path, counters):
