@@ -133,20 +133,26 @@ __device__ __forceinline__ WalkResult walk_meta(const Src& src, const uint8_t* f
 // over the tile records (epoch-tagged granules in p.lb), then writes every block's exclusive
 // base: the output bases are known when the walk ends, with no separate scan launch.  The
 // ticket makes every predecessor tile already running, so the look-back always progresses.
-// STREAM = false: lane b walks block b straight from HBM, one dependent 8-B header load per
+// MODE kWalkGroup (p.wwalk, the default when nblk <= 64 per CU: the lane walk would leave the
+// machine idle): 256 / TB lanes per block guess same-shape runs (see the branch).
+// MODE kWalkLane: lane b walks block b straight from HBM, one dependent 8-B header load per
 // entry (every 128-B line of the input is fetched on its own, as scattered requests).
-// STREAM = true (p.wstream, blocks <= 4 KiB): the tile's blocks go through LDS kSwSub at a time,
+// MODE kWalkStream (p.wwalk, blocks <= 4 KiB): the tile's blocks go through LDS kSwSub at a time,
 // every thread loading one 16-B chunk of each block of the NEXT sub-batch (coalesced, 1 KiB per
 // wave instruction) while wave 0 walks the current one from LDS, one lane per block.  An LDS
 // walk costs ~210 cycles per entry in latency whatever the number of lanes walking
 // (scripts/walk_probe.hip), so it pays when many blocks walk at once and nothing else holds the
 // bytes in LDS -- as here, where the copy is a separate launch.
-template <bool STREAM, uint32_t TB>  // TB = blocks per tile (<= 256 threads: thread t owns block t)
+template <int MODE, uint32_t TB>  // TB = blocks per tile (<= 256 threads: thread t owns block t)
 __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   static_assert(TB <= 256, "one thread per block of the tile");
+  constexpr bool STREAM = MODE == kWalkStream;
   constexpr uint32_t kStageBytes = 256 * kWalkStage * sizeof(uint2);
-  constexpr uint32_t kLdsBytes = STREAM ? kSwSub * kSwSlot : kStageBytes;
-  static_assert(STREAM || kLdsBytes == kStageBytes, "the HBM walk stages 16 records per lane");
+  // group walk: a 32-record ring per block (its LDS also serves the view epilogue's owner map)
+  constexpr uint32_t kLdsBytes = STREAM ? kSwSub * kSwSlot
+                                        : MODE == kWalkGroup ? TB * 32 * sizeof(uint2) : kStageBytes;
+  static_assert(MODE != kWalkLane || kLdsBytes == kStageBytes,
+                "the lane walk stages 16 records per lane");
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   uint2* const stage = reinterpret_cast<uint2*>(lds);
   __shared__ uint32_t s_tile;
@@ -155,7 +161,8 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   __shared__ uint32_t s_first[257];  // p.wfuse: tile-relative first entry of each block
   __shared__ uint32_t s_off[256];    // each block's input offset
   __shared__ uint32_t s_len[STREAM ? 256 : 1];
-  __shared__ uint32_t s_res[STREAM ? 4 : 1][STREAM ? 256 : 1];  // stream walk: n, K, V, status
+  constexpr uint32_t kRes = MODE == kWalkLane ? 1 : 256;
+  __shared__ uint32_t s_res[4][kRes];  // stream / group walk: n, K, V, status per block
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t ntiles = (p.nblk + TB - 1) / TB;
   if (tid == 0) {
@@ -223,6 +230,109 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     if (wave == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (b < p.nblk) {
+      n = s_res[0][tid];
+      K = s_res[1][tid];
+      V = s_res[2][tid];
+      st = s_res[3][tid];
+      uint64_t* t = p.wstat + 3ull * b;
+      t[0] = n;
+      t[1] = K;
+      t[2] = V;
+      p.wstatus[b] = st;
+    }
+  } else if constexpr (MODE == kWalkGroup) {
+    // L lanes per block: each round the group reads the headers at pos + k * stride (stride =
+    // the last accepted entry's size) and accepts the leading run whose guesses were right --
+    // lane k is entry n + k iff entries n .. n + k - 1 all had the previous entry's shape.  The
+    // guessed lines belong to the next entries of the same block (no extra traffic), the group
+    // fetches neighbouring lines together, and the dependent chain shrinks by the run length.
+    constexpr uint32_t L = 256 / TB;
+    static_assert(L >= 2 && L <= 16 && (L & (L - 1)) == 0, "2..16 lanes per block");
+    constexpr uint32_t kMask = (1u << L) - 1;
+    constexpr uint32_t kGroupProbe = 16;
+    const uint32_t g = tid / L, k = tid & (L - 1), gb = lane & ~(L - 1);
+    const uint32_t bg = tile * TB + g;
+    uint2* row = stage + g * 32;  // 32-record ring: a chunk of 16 completes while the next fills
+    if (bg < p.nblk) {
+      const uint32_t off = p.blk_off[bg], len = p.blk_len[bg];
+      uint2* meta = reinterpret_cast<uint2*>(p.wmeta) + (uint64_t)bg * p.wcap;
+      uint32_t pos = 0, gn = 0, gK = 0, gV = 0, gst = LSMGPU_BLK_OK;
+      if ((uint64_t)off + len > p.data_len) {
+        gst = LSMGPU_BLK_RANGE;
+      } else {
+        const uint8_t* blk = p.data + off;
+        uint32_t kref = 0xffffffffu, vref = 0, stride = 0;  // no shape yet: round 1 takes one
+        uint32_t rounds = 0;
+        for (;;) {
+          const uint32_t q = pos + k * stride;  // < 2^21: pos, stride < 2^17, k < 16
+          uint32_t plen = 1, klen = 0, vlen = 0;
+          if (q + 10 <= len) read_hdr(blk + q, plen, klen, vlen);
+          const uint32_t endq = q + 10 + klen + vlen;
+          const bool fast = (klen != 0) & (plen == 0) & (endq <= len);
+          const bool same = fast & (klen == kref) & (vlen == vref);
+          const uint32_t fb = (uint32_t)(__ballot(fast) >> gb) & kMask;
+          const uint32_t sb = (uint32_t)(__ballot(same) >> gb) & kMask;
+          if (!(fb & 1u)) break;  // entry n itself needs the general loop (or the block ended)
+          const uint32_t t = __builtin_ctz(~sb);                          // leading same-shape run
+          const uint32_t m = t + ((t < L && ((fb >> t) & 1u)) ? 1u : 0u);  // + one new shape
+          if (k < m) row[(gn + k) & 31] = make_uint2(q | ((gV + k * vref) << 16), gK + k * kref);
+          const uint32_t src = gb + m - 1;  // the last accepted entry
+          pos = (uint32_t)__shfl((int)endq, (int)src);
+          const uint32_t shape = (uint32_t)__shfl((int)(klen | (vlen << 16)), (int)src);
+          gK += t * kref + (m > t ? (shape & 0xffffu) : 0u);
+          gV += t * vref + (m > t ? (shape >> 16) : 0u);
+          const uint32_t n0 = gn;
+          gn += m;
+          kref = shape & 0xffffu;
+          vref = shape >> 16;
+          stride = 10 + kref + vref;
+          rounds++;
+          if ((n0 ^ gn) & ~15u) {  // chunk [c0, c0 + 16) complete: one full 128-B line
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t c0 = (gn & ~15u) - 16;
+            for (uint32_t i = k; i < 8; i += L) {
+              const uint2 a = row[(c0 + 2 * i) & 31], c = row[(c0 + 2 * i + 1) & 31];
+              reinterpret_cast<uint4*>(meta + c0)[i] = make_uint4(a.x, a.y, c.x, c.y);
+            }
+          }
+          // shapes do not repeat in this block (< 1.25 entries per round after 16 rounds): the
+          // rest entry by entry.  A rate over many rounds, not a streak -- with thousands of
+          // blocks some block always starts unluckily, and the slowest block sets the kernel's
+          // time (C4 shapes, simulated: 2 per round after 8 rounds gives up on 13 % of blocks)
+          if (rounds >= kGroupProbe && 4 * gn < 5 * rounds) break;
+        }
+        if (k == 0) {  // general loop: every stop rule in the iterator's order (as the lane walk)
+          for (;;) {
+            if (pos >= len) break;                                   // iterator.go:115-118
+            if (len - pos < 10) { gst = LSMGPU_BLK_TRUNC_HEADER; break; }
+            uint32_t plen, klen, vlen;
+            read_hdr(blk + pos, plen, klen, vlen);                   // iterator.go:121
+            if ((klen | plen) == 0) break;                           // iterator.go:124-127
+            if (gn == 0 && plen != 0) { gst = LSMGPU_BLK_FIRST_PLEN; break; }  // :129-133
+            if (10 + plen > len) { gst = LSMGPU_BLK_PREFIX_OOB; break; }
+            const uint32_t end = pos + 10 + klen + vlen;             // iterator.go:101-109
+            if (end > len) { gst = LSMGPU_BLK_VALUE_OVERFLOW; break; }
+            row[gn & 31] = make_uint2(pos | (gV << 16), gK);
+            if ((gn & 15) == 15) flush_meta(meta + (gn - 15), row + ((gn - 15) & 31), 16);
+            gK += plen + klen;
+            gV += vlen;
+            gn++;
+            pos = end;
+          }
+        }
+      }
+      if (k == 0) {
+        row[gn & 31] = make_uint2(pos | (gV << 16), gK);  // sentinel
+        flush_meta(meta + (gn & ~15u), row + ((gn & ~15u) & 31), (gn & 15) + 1);
+        s_res[0][g] = gn;
+        s_res[1][g] = gK;
+        s_res[2][g] = gV;
+        s_res[3][g] = gst;
+        s_off[g] = off;
+      }
+    }
+    __syncthreads();
+    if (b < p.nblk) {  // from here on thread t owns block tile * TB + t, as in the other walks
       n = s_res[0][tid];
       K = s_res[1][tid];
       V = s_res[2][tid];
@@ -819,11 +929,17 @@ hipError_t launch_decode_tile(const DecodeParams& p, hipStream_t s) {
 
 hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s) {
   const uint32_t nblk = p.nblk;
-  if (p.wstream)
-    hipLaunchKernelGGL((wsc_walk_kernel<true, kSwTile>), dim3((nblk + kSwTile - 1) / kSwTile),
+  if (p.wwalk == kWalkStream)
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkStream, kSwTile>), dim3((nblk + kSwTile - 1) / kSwTile),
                        dim3(256), 0, s, p);
+  else if (p.wwalk == kWalkGroup && p.wlanes == 4)
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 64>), dim3((nblk + 63) / 64), dim3(256), 0, s, p);
+  else if (p.wwalk == kWalkGroup && p.wlanes == 16)
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 16>), dim3((nblk + 15) / 16), dim3(256), 0, s, p);
+  else if (p.wwalk == kWalkGroup)
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 32>), dim3((nblk + 31) / 32), dim3(256), 0, s, p);
   else
-    hipLaunchKernelGGL((wsc_walk_kernel<false, 256>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 256>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || p.wfuse) return e;  // view-only: the walk wrote everything
   const uint32_t per_wg = 4 / p.wsplit;  // blocks per 4-wave workgroup

@@ -46,7 +46,8 @@ struct DecodeParams {
   uint32_t wj;              // walk-scan-copy: lanes per entry forced (8, 16), 0 = per block
   uint32_t wfuse;           // walk-scan-copy, view-only mode: the walk writes the view index
                             // and per-block outputs itself (no copy launch)
-  uint32_t wstream;         // walk-scan-copy: blocks <= 4 KiB streamed through LDS for the walk
+  uint32_t wwalk;           // walk-scan-copy walk: kWalkLane / kWalkStream / kWalkGroup (+ lanes)
+  uint32_t wlanes;          // kWalkGroup: lanes per block (4, 8 or 16)
 };
 
 // Encode: one wave per output block; every byte position is closed-form
@@ -157,6 +158,10 @@ hipError_t launch_decode_tile(const DecodeParams& p, hipStream_t s);
 // 512-thread workgroups (one per CU, all resident), chunk aggregates in p.lb (epoch-tagged),
 // per-block u32 entry records past the 64 kept in LDS in p.wmeta at stride p.wcap = kFscRec;
 // p.data 16-B aligned, p.data_len >= 16
+// walk-scan-copy walk modes (DecodeParams::wwalk)
+constexpr int kWalkLane = 0;    // one lane per block, header by header from HBM
+constexpr int kWalkStream = 1;  // blocks <= 4 KiB through LDS, walked there
+constexpr int kWalkGroup = 2;   // wlanes lanes per block, speculative same-shape runs from HBM
 constexpr uint32_t kFscRec = 412;  // 409 entries of >= 10 B in 4096 B + the sentinel, rounded
 hipError_t launch_decode_fsc(const DecodeParams& p, int num_cus, hipStream_t s);
 // which decode path a batch takes: 0 register-lag (<= 4 KiB), 1 LDS-lag, 2 walk-scan-copy

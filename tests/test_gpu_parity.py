@@ -499,13 +499,14 @@ def test_wsc_lanes_per_entry(codec, oracle, monkeypatch, lanes):
     _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln), f"J={lanes}")
 
 
-@pytest.mark.parametrize("walk", ["stream", "global"])
+@pytest.mark.parametrize("walk", ["stream", "lane", "group", "group4", "group16"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
-    """Walk-scan-copy's two walks (LSMGPU_WSC_WALK): blocks <= 4 KiB streamed through LDS 16 at a
-    time (the default) or walked lane by lane from HBM.  C2 / C3 blocks, short and tiny entries
-    (> 64 per block), every KAT block (error statuses, terminators, plen > 0) at odd alignments,
-    prefix-compressed random blocks, a ragged last tile and a block ending at the buffer's end."""
+    """Walk-scan-copy's walks (LSMGPU_WSC_WALK): blocks <= 4 KiB streamed through LDS, one lane
+    per block from HBM, or 8 / 4 / 16 lanes per block guessing same-shape runs from HBM.  C2 /
+    C3 blocks, short and tiny entries (> 64 per block), every KAT block (error statuses,
+    terminators, plen > 0) at odd alignments, prefix-compressed random blocks, a ragged last
+    tile and a block ending at the buffer's end (plus C5 32 KiB blocks for the HBM walks)."""
     from lsmdb_amd.codec import MODE_MATERIALIZE, MODE_VIEW
     monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
     monkeypatch.setenv("LSMGPU_WSC_WALK", walk)
@@ -516,6 +517,10 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
              oracle.build_cols(c3.keys, c3.key_end, c3.vs, c3.vs_end, 0, 4096)[0],
              oracle.build_cols(*_random_cols(20000, 25), 0, 4096)[0],
              oracle.build_cols(*_random_cols(60000, 26, 9, 10, 3, 4), 0, 4096)[0]]
+    if walk != "stream":
+        c5 = _cols(5, 6000, seed=27)
+        parts.append(oracle.build_cols(c5.keys, c5.key_end, c5.vs, c5.vs_end, 0,
+                                       c5.block_bytes)[0])
     data, off, ln = _sst_blocks(oracle, parts)
     kd = bytearray(data)
     offs, lens = list(off), list(ln)
