@@ -150,7 +150,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   constexpr uint32_t kStageBytes = 256 * kWalkStage * sizeof(uint2);
   // group walk: a 32-record ring per block (its LDS also serves the view epilogue's owner map)
   constexpr uint32_t kLdsBytes = STREAM ? kSwSub * kSwSlot
-                                        : MODE == kWalkGroup ? TB * 32 * sizeof(uint2) : kStageBytes;
+                                        : MODE == kWalkGroup ? TB * 16 * sizeof(uint2) : kStageBytes;
   static_assert(MODE != kWalkLane || kLdsBytes == kStageBytes,
                 "the lane walk stages 16 records per lane");
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
@@ -159,9 +159,9 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   __shared__ uint32_t s_wave[4][3];
   __shared__ uint32_t s_ex[3];
   __shared__ uint32_t s_first[257];  // p.wfuse: tile-relative first entry of each block
-  __shared__ uint32_t s_off[256];    // each block's input offset
+  __shared__ uint32_t s_off[MODE == kWalkGroup ? TB : 256];  // each block's input offset
   __shared__ uint32_t s_len[STREAM ? 256 : 1];
-  constexpr uint32_t kRes = MODE == kWalkLane ? 1 : 256;
+  constexpr uint32_t kRes = MODE == kWalkLane ? 1 : MODE == kWalkGroup ? TB : 256;
   __shared__ uint32_t s_res[4][kRes];  // stream / group walk: n, K, V, status per block
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t ntiles = (p.nblk + TB - 1) / TB;
@@ -252,7 +252,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     constexpr uint32_t kGroupProbe = 16;
     const uint32_t g = tid / L, k = tid & (L - 1), gb = lane & ~(L - 1);
     const uint32_t bg = tile * TB + g;
-    uint2* row = stage + g * 32;  // 32-record ring: a chunk of 16 completes while the next fills
+    uint2* row = stage + g * 16;  // the block's current 16-record chunk (one 128-B line)
     if (bg < p.nblk) {
       const uint32_t off = p.blk_off[bg], len = p.blk_len[bg];
       uint2* meta = reinterpret_cast<uint2*>(p.wmeta) + (uint64_t)bg * p.wcap;
@@ -275,25 +275,27 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
           if (!(fb & 1u)) break;  // entry n itself needs the general loop (or the block ended)
           const uint32_t t = __builtin_ctz(~sb);                          // leading same-shape run
           const uint32_t m = t + ((t < L && ((fb >> t) & 1u)) ? 1u : 0u);  // + one new shape
-          if (k < m) row[(gn + k) & 31] = make_uint2(q | ((gV + k * vref) << 16), gK + k * kref);
+          const uint2 rec = make_uint2(q | ((gV + k * vref) << 16), gK + k * kref);
+          const uint32_t idx = gn + k, cend = (gn | 15u) + 1;  // end of the current chunk
+          if (k < m && idx < cend) row[idx & 15] = rec;
           const uint32_t src = gb + m - 1;  // the last accepted entry
           pos = (uint32_t)__shfl((int)endq, (int)src);
           const uint32_t shape = (uint32_t)__shfl((int)(klen | (vlen << 16)), (int)src);
           gK += t * kref + (m > t ? (shape & 0xffffu) : 0u);
           gV += t * vref + (m > t ? (shape >> 16) : 0u);
-          const uint32_t n0 = gn;
           gn += m;
           kref = shape & 0xffffu;
           vref = shape >> 16;
           stride = 10 + kref + vref;
           rounds++;
-          if ((n0 ^ gn) & ~15u) {  // chunk [c0, c0 + 16) complete: one full 128-B line
+          if (gn >= cend) {  // chunk [cend - 16, cend) complete: one full 128-B line
             __builtin_amdgcn_wave_barrier();
-            const uint32_t c0 = (gn & ~15u) - 16;
             for (uint32_t i = k; i < 8; i += L) {
-              const uint2 a = row[(c0 + 2 * i) & 31], c = row[(c0 + 2 * i + 1) & 31];
-              reinterpret_cast<uint4*>(meta + c0)[i] = make_uint4(a.x, a.y, c.x, c.y);
+              const uint2 a = row[2 * i], c = row[2 * i + 1];
+              reinterpret_cast<uint4*>(meta + cend - 16)[i] = make_uint4(a.x, a.y, c.x, c.y);
             }
+            __builtin_amdgcn_wave_barrier();  // the chunk is read before the next one fills
+            if (k < m && idx >= cend) row[idx & 15] = rec;
           }
           // shapes do not repeat in this block (< 1.25 entries per round after 16 rounds): the
           // rest entry by entry.  A rate over many rounds, not a streak -- with thousands of
@@ -312,8 +314,8 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
             if (10 + plen > len) { gst = LSMGPU_BLK_PREFIX_OOB; break; }
             const uint32_t end = pos + 10 + klen + vlen;             // iterator.go:101-109
             if (end > len) { gst = LSMGPU_BLK_VALUE_OVERFLOW; break; }
-            row[gn & 31] = make_uint2(pos | (gV << 16), gK);
-            if ((gn & 15) == 15) flush_meta(meta + (gn - 15), row + ((gn - 15) & 31), 16);
+            row[gn & 15] = make_uint2(pos | (gV << 16), gK);
+            if ((gn & 15) == 15) flush_meta(meta + (gn - 15), row, 16);
             gK += plen + klen;
             gV += vlen;
             gn++;
@@ -322,8 +324,8 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
         }
       }
       if (k == 0) {
-        row[gn & 31] = make_uint2(pos | (gV << 16), gK);  // sentinel
-        flush_meta(meta + (gn & ~15u), row + ((gn & ~15u) & 31), (gn & 15) + 1);
+        row[gn & 15] = make_uint2(pos | (gV << 16), gK);  // sentinel
+        flush_meta(meta + (gn & ~15u), row, (gn & 15) + 1);
         s_res[0][g] = gn;
         s_res[1][g] = gK;
         s_res[2][g] = gV;
@@ -932,6 +934,8 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s) {
   if (p.wwalk == kWalkStream)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkStream, kSwTile>), dim3((nblk + kSwTile - 1) / kSwTile),
                        dim3(256), 0, s, p);
+  else if (p.wwalk == kWalkGroup && p.wlanes == 2)
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 128>), dim3((nblk + 127) / 128), dim3(256), 0, s, p);
   else if (p.wwalk == kWalkGroup && p.wlanes == 4)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 64>), dim3((nblk + 63) / 64), dim3(256), 0, s, p);
   else if (p.wwalk == kWalkGroup && p.wlanes == 16)
