@@ -547,3 +547,37 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     so, sl_, _, _ = oracle.parse_index(sst + b"{}" + (2).to_bytes(4, "big"))
     tight = sst[: int(so[-1]) + int(sl_[-1])]
     _assert_same(codec.decode_host(tight, so, sl_), oracle.decode(tight, so, sl_), "tight end")
+
+
+def test_wsc_mixed_copy(codec, oracle, monkeypatch):
+    """Walk-scan-copy's copy over every entry shape in one batch: C2 / C3 blocks, random key
+    and value lengths with zero-length values, > 128 entries per block, prefix-compressed KAT
+    blocks, 32 KiB C5 blocks, blocks at odd offsets, and the last block ending at the buffer's
+    end."""
+    monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
+    c2 = _cols(2, 30000, seed=31)
+    c3 = _cols(3, 2000, seed=32)
+    c5 = _cols(5, 3000, seed=33)
+    parts = [oracle.build_cols(c2.keys, c2.key_end, c2.vs, c2.vs_end, 0, 4096)[0],
+             oracle.build_cols(*_random_cols(20000, 34, 1, 40, 0, 70), 0, 4096)[0],
+             oracle.build_cols(*_random_cols(30000, 35, 1, 3, 0, 2), 0, 4096)[0],
+             oracle.build_cols(c3.keys, c3.key_end, c3.vs, c3.vs_end, 0, 4096)[0],
+             oracle.build_cols(c5.keys, c5.key_end, c5.vs, c5.vs_end, 0, c5.block_bytes)[0]]
+    data, off, ln = _sst_blocks(oracle, parts)
+    kd = bytearray(data)
+    offs, lens = list(off), list(ln)
+    for i, (_n, block, _e, _s) in enumerate(K.DECODE_KATS * 2):
+        kd += b"\xcd" * (i % 11)
+        offs.append(len(kd))
+        lens.append(len(block))
+        kd += block
+    tail = parts[1]
+    to, tl, _, _ = oracle.parse_index(tail + b"{}" + (2).to_bytes(4, "big"))
+    offs += list(to + len(kd))
+    lens += list(tl)
+    kd += tail[: int(to[-1]) + int(tl[-1])]
+    kd = bytes(kd)
+    o2, l2 = np.array(offs, np.uint32), np.array(lens, np.uint32)
+    for sl in (slice(None), slice(None, None, -1), slice(3, None, 7)):
+        oo, ll = np.ascontiguousarray(o2[sl]), np.ascontiguousarray(l2[sl])
+        _assert_same(codec.decode_host(kd, oo, ll), oracle.decode(kd, oo, ll), f"{sl}")
