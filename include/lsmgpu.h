@@ -253,6 +253,31 @@ int lsmgpu_encode_tables_async(lsmgpu_ctx* ctx, const uint8_t* d_keys, const uin
                                uint32_t tables_cap, uint64_t max_blocks, uint8_t* d_out,
                                uint32_t* d_flags);
 
+/* ---- Bloom tail (table/builder.go:164-195 Finish, table/table.go:180-186 readIndex, :301
+ * DoesNotHave) -------------------------------------------------------------------------------
+ * The reference's third-party github.com/AndreasBriese/bbloom v0.0.0-20190825152654-46b345b51c96
+ * restated (DESIGN.md "Bloom tail"; parity of the bbloom-specific bytes unpinned).
+ * lsmgpu_bloom_params: bbloom.New(float64(key_count), 0.01) -> filter bits (a power of two
+ * >= 512), setLocs, and the byte length of its JSONMarshal output (key_count 0: setLocs =
+ * 1 << 63, Go's uint64(NaN) on amd64). */
+int lsmgpu_bloom_params(uint64_t key_count, uint64_t* bits, uint64_t* set_locs, uint64_t* json_len);
+/* Finish's filter: bf.Add(ParseKey(key)) for every key of the batch -- keys WITH their 8-B ts
+ * (what Builder.Add takes), key i = d_keys[d_key_end[i-1], d_key_end[i]).  d_bitset: bits / 64
+ * u64 words, cleared here.  *d_flags |= 1 if a key is <= 8 B (y.go:98 AssertTruef panic; that
+ * key is skipped).  Device pointers, asynchronous on the context's stream. */
+int lsmgpu_bloom_build_async(lsmgpu_ctx* ctx, const uint8_t* d_keys, const uint32_t* d_key_end,
+                             uint64_t n, uint64_t* d_bitset, uint64_t bits, uint64_t set_locs,
+                             uint32_t* d_flags);
+/* bf.JSONMarshal(): {"FilterSet":"<base64 std of the filter bytes>","SetLocs":N}, json_len bytes
+ * (lsmgpu_bloom_params) into d_out (out_cap >= json_len). */
+int lsmgpu_bloom_json_async(lsmgpu_ctx* ctx, const uint64_t* d_bitset, uint64_t bits,
+                            uint64_t set_locs, uint8_t* d_out, uint64_t out_cap);
+/* Table.DoesNotHave for a batch: d_has[i] = bf.Has(key i) (0 = DoesNotHave); keys as the
+ * caller passes them (level_handler.go:221-224 passes ParseKey(key), no ts). */
+int lsmgpu_bloom_has_async(lsmgpu_ctx* ctx, const uint64_t* d_bitset, uint64_t bits,
+                           uint64_t set_locs, const uint8_t* d_keys, const uint32_t* d_key_end,
+                           uint64_t n, uint8_t* d_has);
+
 #ifdef __cplusplus
 }
 #endif

@@ -51,6 +51,10 @@ EXPORTED_SYMBOLS = (
     "lsmgpu_merge_runs_async",
     "lsmgpu_cut_tables_async",
     "lsmgpu_encode_tables_async",
+    "lsmgpu_bloom_params",
+    "lsmgpu_bloom_build_async",
+    "lsmgpu_bloom_json_async",
+    "lsmgpu_bloom_has_async",
     "lsmgpu_decode_blocks",
     "lsmgpu_decode_blocks_async",
     "lsmgpu_encode_blocks",
@@ -191,6 +195,18 @@ def _load() -> ctypes.CDLL:
                                                c_void_p, c_void_p, c_uint32, c_uint64, c_void_p,
                                                c_void_p]
     lib.lsmgpu_encode_tables_async.restype = c_int
+    lib.lsmgpu_bloom_params.argtypes = [c_uint64, POINTER(c_uint64), POINTER(c_uint64),
+                                        POINTER(c_uint64)]
+    lib.lsmgpu_bloom_params.restype = c_int
+    lib.lsmgpu_bloom_build_async.argtypes = [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p,
+                                             c_uint64, c_uint64, c_void_p]
+    lib.lsmgpu_bloom_build_async.restype = c_int
+    lib.lsmgpu_bloom_json_async.argtypes = [c_void_p, c_void_p, c_uint64, c_uint64, c_void_p,
+                                            c_uint64]
+    lib.lsmgpu_bloom_json_async.restype = c_int
+    lib.lsmgpu_bloom_has_async.argtypes = [c_void_p, c_void_p, c_uint64, c_uint64, c_void_p,
+                                           c_void_p, c_uint64, c_void_p]
+    lib.lsmgpu_bloom_has_async.restype = c_int
     return lib
 
 

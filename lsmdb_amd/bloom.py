@@ -1,18 +1,20 @@
-"""bbloom-shaped bloom tail for SSTs built by lsmdb_amd.Builder.
+"""The SST bloom tail's host-side pieces: bbloom.New's sizing and JSONUnmarshal's parse.
 
-The reference writes `bbloom.New(float64(keyCount), 0.01).JSONMarshal()` after the index
-(table/builder.go:164,190-195; AndreasBriese/bbloom v0.0.0-20190825152654-46b345b51c96, not
-vendored, source absent).  Its hash bits are PARITY UNPINNED here.  To stay loadable and safe
-for a Go reader we emit the same JSON shape and filter size with EVERY bit set: Go's
-bbloom.JSONUnmarshal accepts it and `Has` is always true, so `Table.DoesNotHave` never
-excludes a present key (it only loses the filtering).  An exact bbloom restatement is SURVEY
-section 8(f) rank 3.
+The reference writes `bbloom.New(float64(keyCount), 0.01).JSONMarshal()` after the index and
+reads it back with `bbloom.JSONUnmarshal` (table/builder.go:164,189-195, table/table.go:180-186;
+github.com/AndreasBriese/bbloom v0.0.0-20190825152654-46b345b51c96, not vendored).  The filter
+itself -- SipHash-2-4 of every ParseKey(key), setLocs bits per key -- is built and probed on the
+device (csrc/bloom.hip through Codec.bloom_tail_host / Codec.bloom_has_host); DESIGN.md states
+the restated algorithm and its pinning (SipHash core pinned by the published vectors, the
+bbloom-specific bytes "parity unpinned").
 """
 from __future__ import annotations
 
 import base64
 import json
 import math
+
+import numpy as np
 
 LN2 = 0.69314718056  # the constant bbloom uses
 
@@ -34,22 +36,15 @@ def bbloom_params(num_entries: float, wrongs: float = 0.01) -> tuple[int, int]:
     return size, locs
 
 
-def bloom_tail(key_count: int) -> bytes:
-    """JSON bytes of an all-ones bbloom filter sized like bbloom.New(key_count, 0.01)."""
-    size, locs = bbloom_params(float(key_count))
-    filter_set = b"\xff" * (size // 8)
-    doc = {"FilterSet": base64.b64encode(filter_set).decode(), "SetLocs": locs}
-    return json.dumps(doc, separators=(",", ":")).encode()
-
-
-def may_contain(bloom_json: bytes, key: bytes) -> bool:
-    """Table.DoesNotHave's complement.  Exact for all-ones filters; any other filter is
-    answered conservatively (True) because the bbloom hash is not restated (unpinned)."""
+def parse(bloom_json: bytes) -> tuple[np.ndarray, int]:
+    """bbloom.JSONUnmarshal (table/table.go:186): (filter as little-endian u64 words, setLocs).
+    Raises ValueError on a tail Go could not load either."""
     try:
         doc = json.loads(bloom_json)
-        fs = base64.b64decode(doc.get("FilterSet", ""))
-    except Exception:
-        return True
-    if fs and all(b == 0xFF for b in fs):
-        return True
-    return True
+        fs = base64.b64decode(doc["FilterSet"], validate=True)
+        locs = int(doc["SetLocs"])
+    except (ValueError, KeyError, TypeError) as e:
+        raise ValueError(f"bloom tail: {e}") from e
+    if len(fs) < 8 or len(fs) % 8 or (len(fs) & (len(fs) - 1)):
+        raise ValueError("bloom tail: FilterSet is not a power-of-two number of u64 words")
+    return np.frombuffer(fs, dtype="<u8").copy(), locs

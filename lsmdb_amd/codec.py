@@ -432,6 +432,67 @@ class Codec:
                                   o["flags"])
         return o
 
+    # -- bloom tail (table/builder.go:164-195 Finish, table/table.go:301 DoesNotHave)
+    def bloom_build_device(self, keys, key_end, n: int) -> dict:
+        """Finish's filter over n keys WITH ts on the device (asynchronous): device tensors
+        bitset / json / flags plus bits, locs, json_len."""
+        import torch
+        dev = key_end.device
+        bits, locs, jl = bloom_params(n)
+        o = dict(bitset=torch.empty(bits // 64, dtype=torch.int64, device=dev),
+                 json=torch.empty(jl, dtype=torch.uint8, device=dev),
+                 flags=torch.zeros(1, dtype=torch.int32, device=dev),
+                 bits=bits, locs=locs, json_len=jl)
+        check(lib().lsmgpu_bloom_build_async(self._ctx, _ptr(keys), _ptr(key_end), n,
+                                             _ptr(o["bitset"]), bits, locs, _ptr(o["flags"])),
+              "bloom_build_async")
+        check(lib().lsmgpu_bloom_json_async(self._ctx, _ptr(o["bitset"]), bits, locs,
+                                            _ptr(o["json"]), jl), "bloom_json_async")
+        return o
+
+    def bloom_tail_host(self, keys: bytes, key_end: np.ndarray) -> bytes:
+        """bf.JSONMarshal() of Finish's filter for host keys (with ts); raises ValueError for
+        a key of <= 8 B (y.go:98 AssertTruef)."""
+        import torch
+        ke = np.ascontiguousarray(key_end, dtype=np.uint32)
+        n = int(ke.size)
+        kd = torch.from_numpy(np.frombuffer(bytes(keys) + b"\0" * 16, np.uint8).copy()).to(self.device)
+        o = self.bloom_build_device(kd, torch.from_numpy(ke.view(np.int32).copy()).to(self.device), n)
+        self.synchronize()
+        if int(o["flags"].cpu()[0]) & 1:
+            raise ValueError("bloom: a key of <= 8 B (y.go:98 AssertTruef)")
+        return o["json"].cpu().numpy().tobytes()
+
+    def bloom_has_device(self, bitset, bits: int, locs: int, keys, key_end, n: int):
+        """Has(key) for n keys as given (no ts) -> device u8 tensor (asynchronous)."""
+        import torch
+        has = torch.empty(max(n, 1), dtype=torch.uint8, device=key_end.device)
+        check(lib().lsmgpu_bloom_has_async(self._ctx, _ptr(bitset), bits, locs, _ptr(keys),
+                                           _ptr(key_end), n, _ptr(has)), "bloom_has_async")
+        return has
+
+    def bloom_has_host(self, bitset: np.ndarray, locs: int, keys: list) -> np.ndarray:
+        """Table.DoesNotHave's complement for a batch of host keys (no ts): bool array."""
+        import torch
+        bs = np.ascontiguousarray(bitset).view(np.uint64)
+        bits = int(bs.size) * 64
+        ke = np.cumsum([len(k) for k in keys], dtype=np.uint64).astype(np.uint32)
+        n = len(keys)
+        if n == 0:
+            return np.zeros(0, bool)
+        t = lambda a: torch.from_numpy(a.copy()).to(self.device)
+        kd = t(np.frombuffer(b"".join(bytes(k) for k in keys) + b"\0" * 16, np.uint8))
+        has = self.bloom_has_device(t(bs.view(np.int64)), bits, locs, kd, t(ke.view(np.int32)), n)
+        self.synchronize()
+        return has[:n].cpu().numpy().astype(bool)
+
+
+def bloom_params(key_count: int) -> tuple[int, int, int]:
+    """bbloom.New(float64(key_count), 0.01): (filter bits, setLocs, JSONMarshal length)."""
+    bits, locs, jl = c_uint64(), c_uint64(), c_uint64()
+    check(lib().lsmgpu_bloom_params(key_count, byref(bits), byref(locs), byref(jl)), "bloom_params")
+    return bits.value, locs.value, jl.value
+
 
 _DEFAULT: dict[int, Codec] = {}
 

@@ -5,6 +5,8 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -782,3 +784,115 @@ int lsmgpu_encode_tables_async(lsmgpu_ctx* c, const uint8_t* d_keys, const uint3
 }
 
 }  // extern "C"
+
+
+// ---- bloom tail (table/builder.go:164-195, table/table.go:180-186,301; bloom.hip)
+namespace {
+// bbloom.New(n, 0.01): calcSizeByWrongPositives + getSize (float64 exactly as Go evaluates it)
+void bloom_size(uint64_t key_count, uint64_t* bits, uint64_t* locs, uint32_t* exponent) {
+  const double n = (double)key_count, ln2 = 0.69314718056;
+  volatile double l2 = ln2 * ln2;  // math.Pow(0.69314718056, 2): one rounded product
+  const double size = -1 * n * std::log(0.01) / l2;
+  const double lc = std::ceil(ln2 * size / n);
+  *locs = std::isnan(lc) ? (1ull << 63) : (uint64_t)lc;  // Go's uint64(NaN) on amd64
+  uint64_t entries = (uint64_t)size, sz = 1;
+  uint32_t e = 0;
+  if (entries < 512) entries = 512;
+  while (sz < entries) {
+    sz <<= 1;
+    e++;
+  }
+  *bits = sz;
+  *exponent = e;
+}
+int bloom_text(uint64_t set_locs, char* text, uint32_t* head, uint32_t* tail) {
+  static const char kHead[] = "{\"FilterSet\":\"";
+  *head = sizeof kHead - 1;
+  memcpy(text, kHead, *head);
+  const int t = snprintf(text + *head, 64 - *head, "\",\"SetLocs\":%llu}",
+                         (unsigned long long)set_locs);
+  if (t <= 0 || *head + (uint32_t)t >= 64) return LSMGPU_ERR_INTERNAL;
+  *tail = (uint32_t)t;
+  return LSMGPU_OK;
+}
+uint32_t log2_pow2(uint64_t bits) {
+  uint32_t e = 0;
+  while ((1ull << e) < bits) e++;
+  return e;
+}
+bool bloom_bits_ok(uint64_t bits) { return bits >= 512 && (bits & (bits - 1)) == 0 && bits <= (1ull << 40); }
+}  // namespace
+
+int lsmgpu_bloom_params(uint64_t key_count, uint64_t* bits, uint64_t* set_locs, uint64_t* json_len) {
+  if (!bits || !set_locs) return LSMGPU_ERR_ARG;
+  uint32_t e = 0;
+  bloom_size(key_count, bits, set_locs, &e);
+  if (json_len) {
+    char text[64];
+    uint32_t h = 0, t = 0;
+    const int rc = bloom_text(*set_locs, text, &h, &t);
+    if (rc != LSMGPU_OK) return rc;
+    *json_len = h + 4 * ((*bits / 8 + 2) / 3) + t;
+  }
+  return LSMGPU_OK;
+}
+
+int lsmgpu_bloom_build_async(lsmgpu_ctx* c, const uint8_t* d_keys, const uint32_t* d_key_end,
+                             uint64_t n, uint64_t* d_bitset, uint64_t bits, uint64_t set_locs,
+                             uint32_t* d_flags) {
+  if (!c || !d_bitset || !d_flags || !bloom_bits_ok(bits)) return LSMGPU_ERR_ARG;
+  if (n && (!d_keys || !d_key_end)) return LSMGPU_ERR_ARG;
+  if (n > 0xffffffffull) return LSMGPU_ERR_TOO_LARGE;
+  HIPC(hipSetDevice(c->device));
+  HIPC(hipMemsetAsync(d_bitset, 0, bits / 8, c->stream));
+  HIPC(hipMemsetAsync(d_flags, 0, sizeof(uint32_t), c->stream));
+  BloomParams p{};
+  p.keys = d_keys;
+  p.key_end = d_key_end;
+  p.n = n;
+  p.bitset = d_bitset;
+  p.mask = bits - 1;
+  p.locs = set_locs;
+  p.shift = 64 - log2_pow2(bits);
+  p.flags = d_flags;
+  HIPC(launch_bloom_build(p, c->stream));
+  return LSMGPU_OK;
+}
+
+int lsmgpu_bloom_json_async(lsmgpu_ctx* c, const uint64_t* d_bitset, uint64_t bits,
+                            uint64_t set_locs, uint8_t* d_out, uint64_t out_cap) {
+  if (!c || !d_bitset || !d_out || !bloom_bits_ok(bits)) return LSMGPU_ERR_ARG;
+  BloomJson j{};
+  uint32_t h = 0, t = 0;
+  const int rc = bloom_text(set_locs, reinterpret_cast<char*>(j.text), &h, &t);
+  if (rc != LSMGPU_OK) return rc;
+  j.bitset = d_bitset;
+  j.nbytes = bits / 8;
+  j.out = d_out;
+  j.head_len = h;
+  j.tail_len = t;
+  if (out_cap < h + 4 * ((j.nbytes + 2) / 3) + t) return LSMGPU_ERR_CAPACITY;
+  HIPC(hipSetDevice(c->device));
+  HIPC(launch_bloom_json(j, c->stream));
+  return LSMGPU_OK;
+}
+
+int lsmgpu_bloom_has_async(lsmgpu_ctx* c, const uint64_t* d_bitset, uint64_t bits,
+                           uint64_t set_locs, const uint8_t* d_keys, const uint32_t* d_key_end,
+                           uint64_t n, uint8_t* d_has) {
+  if (!c || !d_bitset || !bloom_bits_ok(bits)) return LSMGPU_ERR_ARG;
+  if (n && (!d_keys || !d_key_end || !d_has)) return LSMGPU_ERR_ARG;
+  if (n > 0xffffffffull) return LSMGPU_ERR_TOO_LARGE;
+  HIPC(hipSetDevice(c->device));
+  BloomParams p{};
+  p.keys = d_keys;
+  p.key_end = d_key_end;
+  p.n = n;
+  p.bitset = const_cast<uint64_t*>(d_bitset);
+  p.mask = bits - 1;
+  p.locs = set_locs;
+  p.shift = 64 - log2_pow2(bits);
+  p.has = d_has;
+  HIPC(launch_bloom_has(p, c->stream));
+  return LSMGPU_OK;
+}

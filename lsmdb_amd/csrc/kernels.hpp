@@ -158,6 +158,29 @@ hipError_t launch_decode_tile(const DecodeParams& p, hipStream_t s);
 // 512-thread workgroups (one per CU, all resident), chunk aggregates in p.lb (epoch-tagged),
 // per-block u32 entry records past the 64 kept in LDS in p.wmeta at stride p.wcap = kFscRec;
 // p.data 16-B aligned, p.data_len >= 16
+// bloom tail (bloom.hip; bbloom restated, table/builder.go:164-195, table/table.go:301)
+struct BloomParams {
+  const uint8_t* keys;
+  const uint32_t* key_end;  // running end offsets: key i = keys[key_end[i-1], key_end[i])
+  uint64_t n;
+  uint64_t* bitset;         // bits / 64 little-endian words
+  uint64_t mask;            // bits - 1
+  uint64_t locs;            // setLocs
+  uint32_t shift;           // 64 - log2(bits)
+  uint32_t* flags;          // build: bit 0 = a key of <= 8 B
+  uint8_t* has;             // probe: 1 = Has(key)
+};
+struct BloomJson {
+  const uint64_t* bitset;
+  uint64_t nbytes;          // bits / 8
+  uint8_t* out;
+  uint32_t head_len, tail_len;
+  uint8_t text[64];         // head ++ tail
+};
+hipError_t launch_bloom_build(const BloomParams& p, hipStream_t s);
+hipError_t launch_bloom_has(const BloomParams& p, hipStream_t s);
+hipError_t launch_bloom_json(const BloomJson& p, hipStream_t s);
+
 // walk-scan-copy walk modes (DecodeParams::wwalk)
 constexpr int kWalkLane = 0;    // one lane per block, header by header from HBM
 constexpr int kWalkStream = 1;  // blocks <= 4 KiB through LDS, walked there

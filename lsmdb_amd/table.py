@@ -120,7 +120,7 @@ class Builder:
             vs, vs_end = b"", np.zeros(0, np.uint32)
         body, _data_len, _restarts = codec.encode_host(keys, key_end, vs, vs_end,
                                                        self.entries_per_block, self.block_bytes)
-        bdata = _bloom.bloom_tail(n)
+        bdata = codec.bloom_tail_host(keys, key_end)  # builder.go:164-181,189-195 (device)
         return body + bdata + struct.pack(">I", len(bdata))
 
 
@@ -150,6 +150,8 @@ class Table:
         self.biggest: Optional[bytes] = None
         self.id = 0
         self.bloom_json = b""
+        self._bloom = None  # (bitset, setLocs) once parsed
+        self._codec: Optional[Codec] = None
         self.dec: Optional[HostDecoded] = None
         self._owns_file = False
 
@@ -184,8 +186,16 @@ class Table:
         return self.id
 
     def DoesNotHave(self, key: bytes) -> bool:  # noqa: N802
-        """table.go:301 (bbloom hash unpinned: conservative, see bloom.py)."""
-        return not _bloom.may_contain(self.bloom_json, key)
+        """table.go:301: !bf.Has(key), probed on the device (key as the caller passes it:
+        level_handler.go:221-224 strips the ts first)."""
+        return bool(self.DoesNotHaveBatch([key])[0])
+
+    def DoesNotHaveBatch(self, keys) -> np.ndarray:  # noqa: N802
+        """DoesNotHave for many keys in one device probe: bool array (True = not present)."""
+        if self._bloom is None:
+            self._bloom = _bloom.parse(self.bloom_json)  # table.go:186 JSONUnmarshal
+        bitset, locs = self._bloom
+        return ~(self._codec or default_codec()).bloom_has_host(bitset, locs, list(keys))
 
     def NewIterator(self, reversed: bool) -> "Iterator":  # noqa: N802
         return Iterator(self, reversed)
@@ -236,6 +246,7 @@ def OpenTable(path_or_bytes, loading_mode: int = MEMORY_MAP, codec: Optional[Cod
     without a GPU."""
     t = Table()
     t.loading_mode = loading_mode
+    t._codec = codec
     if isinstance(path_or_bytes, (bytes, bytearray, memoryview)):
         raw = bytes(path_or_bytes)
         t.id = file_id or 0

@@ -16,7 +16,8 @@
  * cannot be executed here or on the GPU box.  The oracle is pinned by (1) the reference's
  * own known answers in table/table_test.go (counts, value order, Meta, seek tables) and
  * (2) byte-level KATs hand-derived from table/builder.go (tests/golden/kat.json).  The
- * bloom tail (third-party bbloom, not vendored) is out of the oracle: "parity unpinned".
+ * bloom tail (third-party bbloom, not vendored) is restated in bbloom.c: its SipHash core is
+ * pinned by the published test vector, the rest is "parity unpinned" (see bbloom.c).
  */
 #ifndef SSTREF_H
 #define SSTREF_H
@@ -147,6 +148,21 @@ int sstref_open_table(const uint8_t* sst, size_t len, uint32_t* blk_off, uint32_
  * (or (size_t)-1 if cap is too small). */
 size_t sstref_merge(const uint8_t* kd, const uint32_t* ke, const uint32_t* run_first,
                     size_t nruns, uint32_t* out_src, size_t cap);
+
+/* ---- bloom tail (bbloom.c: AndreasBriese/bbloom v0.0.0-20190825152654-46b345b51c96 restated;
+ *      table/builder.go:164-195, table/table.go:180-186,301) ---- */
+uint64_t sstref_siphash24(uint64_t k0, uint64_t k1, const uint8_t* p, size_t n);
+void   sstref_bloom_params(double num_entries, double wrongs, uint64_t* size_bits,
+                           uint64_t* set_locs, uint32_t* exponent);
+void   sstref_bloom_add(uint64_t* bitset, uint64_t size_bits, uint32_t exponent,
+                        uint64_t set_locs, const uint8_t* key, size_t n);
+int    sstref_bloom_has(const uint64_t* bitset, uint64_t size_bits, uint32_t exponent,
+                        uint64_t set_locs, const uint8_t* key, size_t n);
+size_t sstref_bloom_json(const uint64_t* bitset, uint64_t size_bits, uint64_t set_locs,
+                         uint8_t* out, size_t cap);
+int    sstref_bloom_build(const uint8_t* keys, const uint32_t* key_end, size_t n,
+                          uint64_t* bitset, uint64_t size_bits, uint32_t exponent,
+                          uint64_t set_locs);
 
 /* ---- y/y.go key helpers ---- */
 int sstref_compare_keys(const uint8_t* k1, size_t l1, const uint8_t* k2, size_t l2); /* y.go:84-90 */

@@ -74,6 +74,17 @@ def lib():
         L.sstref_decode_bench.restype = ctypes.c_double
         L.sstref_compare_keys.argtypes = [c_void_p, c_size_t, c_void_p, c_size_t]
         L.sstref_compare_keys.restype = c_int
+        L.sstref_siphash24.argtypes = [c_uint64, c_uint64, c_void_p, c_size_t]
+        L.sstref_siphash24.restype = c_uint64
+        L.sstref_bloom_params.argtypes = [ctypes.c_double, ctypes.c_double, POINTER(c_uint64),
+                                          POINTER(c_uint64), POINTER(c_uint32)]
+        L.sstref_bloom_has.argtypes = [c_void_p, c_uint64, c_uint32, c_uint64, c_void_p, c_size_t]
+        L.sstref_bloom_has.restype = c_int
+        L.sstref_bloom_json.argtypes = [c_void_p, c_uint64, c_uint64, c_void_p, c_size_t]
+        L.sstref_bloom_json.restype = c_size_t
+        L.sstref_bloom_build.argtypes = [c_void_p, c_void_p, c_size_t, c_void_p, c_uint64, c_uint32,
+                                         c_uint64]
+        L.sstref_bloom_build.restype = c_int
         L.sstref_open_table.argtypes = [c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_size_t, POINTER(TableInfo)]
         L.sstref_open_table.restype = c_int
@@ -247,3 +258,40 @@ def merge(key_data, key_end, run_first) -> np.ndarray:
     n = lib().sstref_merge(_p(kd), _p(ke), _p(rf), rf.size - 1, _p(out), out.size)
     assert n != ctypes.c_size_t(-1).value
     return out[:n].copy()
+
+
+# ---- bloom tail (oracle/bbloom.c: bbloom restated; table/builder.go:164-195)
+def siphash24(k0: int, k1: int, msg: bytes) -> int:
+    b = _u8(msg)
+    return int(lib().sstref_siphash24(k0, k1, _p(b), len(msg)))
+
+
+def bloom_params(n: int, wrongs: float = 0.01) -> tuple[int, int, int]:
+    """(size in bits, setLocs, exponent) of bbloom.New(float64(n), wrongs)."""
+    sz, locs, ex = c_uint64(), c_uint64(), c_uint32()
+    lib().sstref_bloom_params(float(n), wrongs, byref(sz), byref(locs), byref(ex))
+    return sz.value, locs.value, ex.value
+
+
+def bloom_build(keys: bytes, key_end: np.ndarray) -> tuple[np.ndarray, int, int, int]:
+    """Finish's filter over keys WITH ts (ParseKey strips 8 B): (bitset u64, bits, locs, exp)."""
+    ke = np.ascontiguousarray(key_end, np.uint32)
+    bits, locs, ex = bloom_params(ke.size)
+    bs = np.zeros(bits // 64, np.uint64)
+    kb = _u8(keys)
+    rc = lib().sstref_bloom_build(_p(kb), _p(ke), ke.size, _p(bs), bits, ex, locs)
+    if rc != 0:
+        raise ValueError("key of <= 8 B (y.go:98)")
+    return bs, bits, locs, ex
+
+
+def bloom_has(bitset: np.ndarray, bits: int, locs: int, ex: int, key: bytes) -> bool:
+    kb = _u8(key)
+    return bool(lib().sstref_bloom_has(_p(bitset), bits, ex, locs, _p(kb), len(key)))
+
+
+def bloom_json(bitset: np.ndarray, bits: int, locs: int) -> bytes:
+    n = int(lib().sstref_bloom_json(_p(bitset), bits, locs, None, 0))
+    out = np.zeros(n, np.uint8)
+    lib().sstref_bloom_json(_p(bitset), bits, locs, _p(out), n)
+    return out.tobytes()

@@ -36,7 +36,9 @@ class CpuEnv:
         keys = [key_with_ts(k.encode(), 0) for k, _ in kvs]
         vss = [ValueStruct(meta=ord("A"), value=v.encode()).encode() for _, v in kvs]
         body, _, _ = self.o.build(keys, vss, entries_per_block=100)
-        bd = bloom.bloom_tail(len(kvs))
+        kb, ke = self.o.columns(keys, vss)[:2]
+        bs, bits, locs, _ = self.o.bloom_build(kb, ke)
+        bd = self.o.bloom_json(bs, bits, locs)
         return body + bd + struct.pack(">I", len(bd))
 
     def open(self, raw: bytes, mode: int = T.MEMORY_MAP):

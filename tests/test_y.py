@@ -4,6 +4,8 @@ import json
 import base64
 import time
 
+import numpy as np
+
 import pytest
 
 from lsmdb_amd import bloom
@@ -161,17 +163,22 @@ def test_key_helpers():
         compare_keys(b"short", b"alsoshort")
 
 
-@pytest.mark.parametrize("n", [0, 1, 2, 100, 10000, 519540])
-def test_bloom_tail_shape(n):
-    raw = bloom.bloom_tail(n)
+@pytest.mark.parametrize("n", [0, 1, 2, 100, 10000])
+def test_bloom_tail_parse(oracle, n):
+    """bloom.parse (JSONUnmarshal, table.go:186) reads back the oracle's JSONMarshal exactly,
+    and the host sizing agrees with bbloom.New's."""
+    rng = np.random.default_rng(n)
+    ln = rng.integers(9, 30, n)
+    kb = rng.integers(0, 256, int(ln.sum()), dtype=np.uint8).tobytes()
+    bs, bits, locs, _ = oracle.bloom_build(kb, np.cumsum(ln).astype(np.uint32))
+    raw = oracle.bloom_json(bs, bits, locs)
     doc = json.loads(raw)
     assert list(doc) == ["FilterSet", "SetLocs"]
-    fs = base64.b64decode(doc["FilterSet"])
-    size, locs = bloom.bbloom_params(float(n))
-    assert len(fs) * 8 == size and size >= 512 and (size & (size - 1)) == 0
-    assert doc["SetLocs"] == locs
-    assert all(b == 0xFF for b in fs)
-    assert bloom.may_contain(raw, b"anything")
+    got, glocs = bloom.parse(raw)
+    assert np.array_equal(got, bs) and glocs == locs
+    assert bloom.bbloom_params(float(n)) == (bits, locs)
+    with pytest.raises(ValueError):
+        bloom.parse(b'{"FilterSet":"AAA","SetLocs":7}')
 
 
 class _RawIterator:
