@@ -74,11 +74,20 @@ __global__ void __launch_bounds__(256) bloom_build_kernel(BloomParams p) {
   const uint8_t* k = p.keys + s;
   // the key's last word is followed by its 8-B ts: a whole 8-B read never leaves key i
   const uint64_t hash = bbloom_sip(k, e - s - 8, k + (e - s));
+  // equal hashes set equal bits: a lane whose hash equals the wave's first active lane's
+  // leaves the bits to that lane (keys sharing ParseKey(key) -- e.g. 16-B keys without a ts,
+  // whose first 8 B repeat -- would otherwise serialize on the same words' atomics)
+  const uint32_t lo = (uint32_t)hash, hi = (uint32_t)(hash >> 32);
+  const bool same = __builtin_amdgcn_readfirstlane(lo) == lo && __builtin_amdgcn_readfirstlane(hi) == hi;
+  if (same && __lane_id() != (uint32_t)__builtin_ctzll(__ballot(1))) return;
   const uint64_t h = hash >> p.shift, l = (hash << p.shift) >> p.shift;
   unsigned long long* w = reinterpret_cast<unsigned long long*>(p.bitset);
   for (uint64_t j = 0; j < p.locs; j++) {
     const uint64_t idx = (h + j * l) & p.mask;
-    atomicOr(w + (idx >> 6), 1ull << (idx & 63));
+    const unsigned long long bit = 1ull << (idx & 63);
+    // a bit another key already set needs no atomic (a stale read only costs the atomic)
+    if (!(__hip_atomic_load(w + (idx >> 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit))
+      atomicOr(w + (idx >> 6), bit);
   }
 }
 
