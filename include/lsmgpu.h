@@ -241,6 +241,14 @@ int lsmgpu_cut_tables_async(lsmgpu_ctx* ctx, const uint32_t* d_key_end, const ui
                             uint64_t n, uint32_t entries_per_block, int64_t cap,
                             uint32_t* d_tbl_first, uint32_t* d_tbl_blk, uint64_t* d_tbl_out,
                             uint32_t tables_cap, uint64_t* d_result);
+/* The same cut; flags LSMGPU_CUT_BLOOM also reserves each table's bloom tail (Finish's
+ * bbloom JSON + BE32 length, table/builder.go:189-195) after its index, so tbl_out / the image
+ * bytes describe complete .sst files once lsmgpu_bloom_tables_async has filled the tails. */
+#define LSMGPU_CUT_BLOOM 1u
+int lsmgpu_cut_tables_ex_async(lsmgpu_ctx* ctx, const uint32_t* d_key_end, const uint32_t* d_vs_end,
+                               uint64_t n, uint32_t entries_per_block, int64_t cap, uint32_t flags,
+                               uint32_t* d_tbl_first, uint32_t* d_tbl_blk, uint64_t* d_tbl_out,
+                               uint32_t tables_cap, uint64_t* d_result);
 /* Encodes every table of a cut (one launch over all their blocks) into d_out (sized for the
  * cut's image bytes).  max_blocks bounds the tables' total block count (grid size), e.g.
  * ceil(n / entries_per_block) + tables_cap.  key_total / vs_total (0 if unknown) pick the lanes
@@ -277,6 +285,18 @@ int lsmgpu_bloom_json_async(lsmgpu_ctx* ctx, const uint64_t* d_bitset, uint64_t 
 int lsmgpu_bloom_has_async(lsmgpu_ctx* ctx, const uint64_t* d_bitset, uint64_t bits,
                            uint64_t set_locs, const uint8_t* d_keys, const uint32_t* d_key_end,
                            uint64_t n, uint8_t* d_has);
+
+/* Finish's bloom tail for every table of a LSMGPU_CUT_BLOOM cut (after
+ * lsmgpu_encode_tables_async): table t's filter over ParseKey of its keys (entries
+ * [tbl_first[t], tbl_first[t+1]) of the stream) and JSON ++ BE32(len) into the last bytes of
+ * [tbl_out[t], tbl_out[t+1]) of d_out.  tbl_first / tbl_out are HOST copies of the cut's
+ * arrays (ntables + 1 each); d_scratch holds the filters of 32 tables side by side (the sum
+ * of bits / 64 words over each group of 32 consecutive tables, lsmgpu_bloom_params).
+ * *d_flags |= 1 for a key of <= 8 B.  Asynchronous: one memset + 2 launches per 32 tables. */
+int lsmgpu_bloom_tables_async(lsmgpu_ctx* ctx, const uint8_t* d_keys, const uint32_t* d_key_end,
+                              const uint32_t* tbl_first, const uint64_t* tbl_out, uint32_t ntables,
+                              uint8_t* d_out, uint64_t* d_scratch, uint64_t scratch_words,
+                              uint32_t* d_flags);
 
 #ifdef __cplusplus
 }

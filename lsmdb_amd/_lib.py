@@ -55,6 +55,8 @@ EXPORTED_SYMBOLS = (
     "lsmgpu_bloom_build_async",
     "lsmgpu_bloom_json_async",
     "lsmgpu_bloom_has_async",
+    "lsmgpu_cut_tables_ex_async",
+    "lsmgpu_bloom_tables_async",
     "lsmgpu_decode_blocks",
     "lsmgpu_decode_blocks_async",
     "lsmgpu_encode_blocks",
@@ -207,6 +209,13 @@ def _load() -> ctypes.CDLL:
     lib.lsmgpu_bloom_has_async.argtypes = [c_void_p, c_void_p, c_uint64, c_uint64, c_void_p,
                                            c_void_p, c_uint64, c_void_p]
     lib.lsmgpu_bloom_has_async.restype = c_int
+    lib.lsmgpu_cut_tables_ex_async.argtypes = [c_void_p, c_void_p, c_void_p, c_uint64, c_uint32,
+                                               ctypes.c_int64, c_uint32, c_void_p, c_void_p,
+                                               c_void_p, c_uint32, c_void_p]
+    lib.lsmgpu_cut_tables_ex_async.restype = c_int
+    lib.lsmgpu_bloom_tables_async.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                              c_uint32, c_void_p, c_void_p, c_uint64, c_void_p]
+    lib.lsmgpu_bloom_tables_async.restype = c_int
     return lib
 
 

@@ -387,9 +387,9 @@ class Codec:
 
     # -- compaction output tables (Builder.ReachedCapacity cut + one encode over every table)
     def cut_tables_device(self, key_end, vs_end, n: int, cap: int, entries_per_block: int = 100,
-                          tables_cap: int = 4096) -> dict:
-        """lsmgpu_cut_tables_async (asynchronous): device tensors tbl_first / tbl_blk /
-        tbl_out / result."""
+                          tables_cap: int = 4096, bloom: bool = False) -> dict:
+        """lsmgpu_cut_tables_ex_async (asynchronous): device tensors tbl_first / tbl_blk /
+        tbl_out / result; bloom=True reserves each table's bloom tail (complete .sst files)."""
         import torch
         dev = key_end.device
         o = dict(tbl_first=torch.empty(tables_cap + 1, dtype=torch.int32, device=dev),
@@ -397,11 +397,31 @@ class Codec:
                  tbl_out=torch.empty(tables_cap + 1, dtype=torch.int64, device=dev),
                  result=torch.zeros(8, dtype=torch.int64, device=dev),
                  tables_cap=tables_cap, epb=entries_per_block, n=n)
-        check(lib().lsmgpu_cut_tables_async(self._ctx, _ptr(key_end), _ptr(vs_end), n,
-                                            entries_per_block, cap, _ptr(o["tbl_first"]),
-                                            _ptr(o["tbl_blk"]), _ptr(o["tbl_out"]), tables_cap,
-                                            _ptr(o["result"])), "cut_tables_async")
+        check(lib().lsmgpu_cut_tables_ex_async(self._ctx, _ptr(key_end), _ptr(vs_end), n,
+                                               entries_per_block, cap, 1 if bloom else 0,
+                                               _ptr(o["tbl_first"]), _ptr(o["tbl_blk"]),
+                                               _ptr(o["tbl_out"]), tables_cap, _ptr(o["result"])),
+              "cut_tables_ex_async")
+        o["bloom"] = bloom
         return o
+
+    def bloom_tables_device(self, cut: dict, keys, key_end, out, flags) -> None:
+        """Fill the bloom tails of a bloom=True cut's tables (after encode_tables_device);
+        reads the cut's small tbl_first / tbl_out arrays back to the host (synchronizes)."""
+        import torch
+        nt = int(cut["ntables"])
+        if "bloom_host" not in cut:  # the cut's arrays on the host, once
+            tf = cut["tbl_first"][: nt + 1].cpu().numpy().view(np.uint32).copy()
+            to = cut["tbl_out"][: nt + 1].cpu().numpy().view(np.uint64).copy()
+            per = [bloom_params(int(tf[t + 1] - tf[t]))[0] // 64 for t in range(nt)]
+            words = max([sum(per[g: g + 32]) for g in range(0, nt, 32)], default=8)
+            # the scratch stays alive with the cut (the stream may still be using it)
+            cut["bloom_host"] = (tf, to, words,
+                                 torch.empty(words, dtype=torch.int64, device=key_end.device))
+        tf, to, words, scratch = cut["bloom_host"]
+        check(lib().lsmgpu_bloom_tables_async(self._ctx, _ptr(keys), _ptr(key_end), _ptr(tf),
+                                              _ptr(to), nt, _ptr(out), _ptr(scratch), words,
+                                              _ptr(flags)), "bloom_tables_async")
 
     def encode_tables_device(self, cut: dict, keys, key_end, vs, vs_end, key_total: int,
                              vs_total: int, out, flags) -> None:
@@ -415,12 +435,13 @@ class Codec:
 
     def compact_tables_device(self, keys, key_end, vs, vs_end, n: int, key_total: int,
                               vs_total: int, cap: int, entries_per_block: int = 100,
-                              tables_cap: int = 4096) -> dict:
+                              tables_cap: int = 4096, bloom: bool = False) -> dict:
         """Cut the sorted stream into compactBuildTables' output tables and encode them all;
         synchronizes once to size the output.  Returns device tensors: out (images back to
-        back), tbl_first / tbl_blk / tbl_out, result, flags."""
+        back -- complete .sst files with bloom=True), tbl_first / tbl_blk / tbl_out, result,
+        flags (bloom: bloom_flags)."""
         import torch
-        o = self.cut_tables_device(key_end, vs_end, n, cap, entries_per_block, tables_cap)
+        o = self.cut_tables_device(key_end, vs_end, n, cap, entries_per_block, tables_cap, bloom)
         self.synchronize()
         r = o["result"].cpu().numpy()
         if r[3]:
@@ -430,6 +451,9 @@ class Codec:
         o["flags"] = torch.zeros(4, dtype=torch.int32, device=key_end.device)
         self.encode_tables_device(o, keys, key_end, vs, vs_end, key_total, vs_total, o["out"],
                                   o["flags"])
+        if bloom:
+            o["bloom_flags"] = torch.zeros(1, dtype=torch.int32, device=key_end.device)
+            self.bloom_tables_device(o, keys, key_end, o["out"], o["bloom_flags"])
         return o
 
     # -- bloom tail (table/builder.go:164-195 Finish, table/table.go:301 DoesNotHave)

@@ -729,6 +729,15 @@ int lsmgpu_cut_tables_async(lsmgpu_ctx* c, const uint32_t* d_key_end, const uint
                             uint64_t n, uint32_t entries_per_block, int64_t cap,
                             uint32_t* d_tbl_first, uint32_t* d_tbl_blk, uint64_t* d_tbl_out,
                             uint32_t tables_cap, uint64_t* d_result) {
+  return lsmgpu_cut_tables_ex_async(c, d_key_end, d_vs_end, n, entries_per_block, cap, 0,
+                                    d_tbl_first, d_tbl_blk, d_tbl_out, tables_cap, d_result);
+}
+
+int lsmgpu_cut_tables_ex_async(lsmgpu_ctx* c, const uint32_t* d_key_end, const uint32_t* d_vs_end,
+                               uint64_t n, uint32_t entries_per_block, int64_t cap, uint32_t flags,
+                               uint32_t* d_tbl_first, uint32_t* d_tbl_blk, uint64_t* d_tbl_out,
+                               uint32_t tables_cap, uint64_t* d_result) {
+  if (flags & ~(uint32_t)LSMGPU_CUT_BLOOM) return LSMGPU_ERR_ARG;
   if (!c || !d_tbl_first || !d_tbl_blk || !d_tbl_out || !d_result) return LSMGPU_ERR_ARG;
   if (n && (!d_key_end || !d_vs_end)) return LSMGPU_ERR_ARG;
   if (entries_per_block == 0 || tables_cap == 0) return LSMGPU_ERR_ARG;
@@ -746,6 +755,11 @@ int lsmgpu_cut_tables_async(lsmgpu_ctx* c, const uint32_t* d_key_end, const uint
   p.tbl_out = d_tbl_out;
   p.tables_cap = tables_cap;
   p.result = d_result;
+  p.bloom = (flags & LSMGPU_CUT_BLOOM) != 0;
+  p.logw = std::log(0.01);
+  p.ln2 = 0.69314718056;
+  volatile double l2 = p.ln2 * p.ln2;  // math.Pow(0.69314718056, 2): one rounded product
+  p.ln2sq = l2;
   HIPC(launch_cut_tables(p, c->stream));
   return LSMGPU_OK;
 }
@@ -811,7 +825,7 @@ int bloom_text(uint64_t set_locs, char* text, uint32_t* head, uint32_t* tail) {
   memcpy(text, kHead, *head);
   const int t = snprintf(text + *head, 64 - *head, "\",\"SetLocs\":%llu}",
                          (unsigned long long)set_locs);
-  if (t <= 0 || *head + (uint32_t)t >= 64) return LSMGPU_ERR_INTERNAL;
+  if (t <= 0 || *head + (uint32_t)t + 4 > 64) return LSMGPU_ERR_INTERNAL;  // room for a BE32
   *tail = (uint32_t)t;
   return LSMGPU_OK;
 }
@@ -894,5 +908,57 @@ int lsmgpu_bloom_has_async(lsmgpu_ctx* c, const uint64_t* d_bitset, uint64_t bit
   p.shift = 64 - log2_pow2(bits);
   p.has = d_has;
   HIPC(launch_bloom_has(p, c->stream));
+  return LSMGPU_OK;
+}
+
+int lsmgpu_bloom_tables_async(lsmgpu_ctx* c, const uint8_t* d_keys, const uint32_t* d_key_end,
+                              const uint32_t* tbl_first, const uint64_t* tbl_out, uint32_t ntables,
+                              uint8_t* d_out, uint64_t* d_scratch, uint64_t scratch_words,
+                              uint32_t* d_flags) {
+  if (!c || !tbl_first || !tbl_out || !d_out || !d_scratch || !d_flags) return LSMGPU_ERR_ARG;
+  if (ntables && (!d_keys || !d_key_end)) return LSMGPU_ERR_ARG;
+  HIPC(hipSetDevice(c->device));
+  HIPC(hipMemsetAsync(d_flags, 0, sizeof(uint32_t), c->stream));
+  // up to kBloomSegs tables per launch pair, their filters side by side in the scratch
+  for (uint32_t t0 = 0; t0 < ntables; t0 += kBloomSegs) {
+    const uint32_t nseg = std::min<uint32_t>(kBloomSegs, ntables - t0);
+    BloomTables p{};
+    p.keys = d_keys;
+    p.key_end = d_key_end;
+    p.scratch = d_scratch;
+    p.out = d_out;
+    p.flags = d_flags;
+    p.nseg = nseg;
+    p.end = tbl_first[t0 + nseg];
+    uint64_t words = 0, groups = 0;
+    for (uint32_t k = 0; k < nseg; k++) {
+      const uint32_t t = t0 + k;
+      const uint64_t cnt = tbl_first[t + 1] - tbl_first[t];
+      if (cnt == 0 || tbl_first[t + 1] < tbl_first[t] || tbl_out[t + 1] < tbl_out[t])
+        return LSMGPU_ERR_ARG;
+      uint64_t bits = 0, locs = 0, jl = 0;
+      int rc = lsmgpu_bloom_params(cnt, &bits, &locs, &jl);
+      if (rc != LSMGPU_OK) return rc;
+      if (tbl_out[t + 1] - tbl_out[t] < jl + 4 || locs > 0xffffffffull) return LSMGPU_ERR_CAPACITY;
+      BloomSeg& sg = p.seg[k];
+      sg.word_off = words;
+      sg.mask = bits - 1;
+      sg.json_out = tbl_out[t + 1] - jl - 4;
+      sg.group_off = groups;
+      sg.first = tbl_first[t];
+      sg.shift = 64 - log2_pow2(bits);
+      sg.locs = (uint32_t)locs;
+      const int tl = snprintf(reinterpret_cast<char*>(sg.tail), sizeof sg.tail, "\",\"SetLocs\":%llu}",
+                              (unsigned long long)locs);
+      if (tl <= 0 || (uint32_t)tl + 4 > sizeof sg.tail) return LSMGPU_ERR_INTERNAL;
+      for (int b = 0; b < 4; b++) sg.tail[tl + b] = (uint8_t)(jl >> (24 - 8 * b));  // bloomLen
+      sg.tail_len = (uint32_t)tl + 4;
+      words += bits / 64;
+      groups += (bits / 8 + 2) / 3;
+    }
+    if (words > scratch_words) return LSMGPU_ERR_CAPACITY;
+    HIPC(hipMemsetAsync(d_scratch, 0, words * 8, c->stream));
+    HIPC(launch_bloom_tables(p, groups, c->stream));
+  }
   return LSMGPU_OK;
 }

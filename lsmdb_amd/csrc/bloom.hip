@@ -66,7 +66,7 @@ __device__ __forceinline__ uint64_t bbloom_sip(const uint8_t* p, uint32_t n, con
 __global__ void __launch_bounds__(256) bloom_build_kernel(BloomParams p) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= p.n) return;
-  const uint32_t s = i ? p.key_end[i - 1] : 0, e = p.key_end[i];
+  const uint32_t s = i ? p.key_end[i - 1] : (p.key_base ? *p.key_base : 0u), e = p.key_end[i];
   if (e - s <= 8 || e < s) {  // y.go:98 AssertTruef(len(key) > 8): a panic in Go
     atomicOr(p.flags, 1u);
     return;
@@ -133,7 +133,92 @@ __global__ void __launch_bounds__(256) bloom_json_kernel(BloomJson p) {
   }
 }
 
+// ---- many tables at once (compaction: Finish for every output table)
+__device__ __forceinline__ uint32_t seg_of_key(const BloomTables& p, uint32_t i) {
+  uint32_t lo = 0, hi = p.nseg - 1;  // largest t with seg[t].first <= i
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (p.seg[mid].first <= i) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(256) bloom_tables_build_kernel(BloomTables p) {
+  const uint64_t gi = (uint64_t)blockIdx.x * 256 + threadIdx.x + p.seg[0].first;
+  if (gi >= p.end) return;
+  const uint32_t i = (uint32_t)gi;
+  const BloomSeg& sg = p.seg[seg_of_key(p, i)];
+  const uint32_t s = i ? p.key_end[i - 1] : 0u, e = p.key_end[i];
+  if (e - s <= 8 || e < s) {  // y.go:98 AssertTruef(len(key) > 8)
+    atomicOr(p.flags, 1u);
+    return;
+  }
+  const uint8_t* k = p.keys + s;
+  const uint64_t hash = bbloom_sip(k, e - s - 8, k + (e - s));
+  const uint32_t lo32 = (uint32_t)hash, hi32 = (uint32_t)(hash >> 32);
+  const uint64_t wo = sg.word_off;
+  // lanes repeating the first active lane's hash in the same table leave the bits to it
+  const bool same = __builtin_amdgcn_readfirstlane(lo32) == lo32 &&
+                    __builtin_amdgcn_readfirstlane(hi32) == hi32 &&
+                    __builtin_amdgcn_readfirstlane((uint32_t)wo) == (uint32_t)wo;
+  if (same && __lane_id() != (uint32_t)__builtin_ctzll(__ballot(1))) return;
+  const uint64_t h = hash >> sg.shift, l = (hash << sg.shift) >> sg.shift;
+  unsigned long long* w = reinterpret_cast<unsigned long long*>(p.scratch + wo);
+  for (uint32_t j = 0; j < sg.locs; j++) {
+    const uint64_t idx = (h + (uint64_t)j * l) & sg.mask;
+    const unsigned long long bit = 1ull << (idx & 63);
+    if (!(__hip_atomic_load(w + (idx >> 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit))
+      atomicOr(w + (idx >> 6), bit);
+  }
+}
+
+// thread g < groups: 4 base64 characters of its table; then 64 threads per table write the
+// head / tail text bytes
+__global__ void __launch_bounds__(256) bloom_tables_json_kernel(BloomTables p, uint64_t groups) {
+  const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  static constexpr char kHead[] = "{\"FilterSet\":\"";
+  if (g < groups) {
+    uint32_t lo = 0, hi = p.nseg - 1;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (p.seg[mid].group_off <= g) lo = mid; else hi = mid - 1;
+    }
+    const BloomSeg& sg = p.seg[lo];
+    const uint64_t gl = g - sg.group_off, nbytes = (sg.mask + 1) / 8, i = 3 * gl;
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(p.scratch + sg.word_off);
+    const uint32_t a = src[i], b = i + 1 < nbytes ? src[i + 1] : 0u, c = i + 2 < nbytes ? src[i + 2] : 0u;
+    const uint32_t w = (a << 16) | (b << 8) | c;
+    auto enc = [](uint32_t x) -> uint8_t {
+      return (uint8_t)(x < 26 ? 'A' + x : x < 52 ? 'a' + (x - 26) : x < 62 ? '0' + (x - 52) : x == 62 ? '+' : '/');
+    };
+    uint8_t* o = p.out + sg.json_out + 14 + 4 * gl;
+    o[0] = enc((w >> 18) & 63);
+    o[1] = enc((w >> 12) & 63);
+    o[2] = i + 1 < nbytes ? enc((w >> 6) & 63) : (uint8_t)'=';
+    o[3] = i + 2 < nbytes ? enc(w & 63) : (uint8_t)'=';
+  } else if (g < groups + 64ull * p.nseg) {
+    const uint32_t t = (uint32_t)((g - groups) >> 6), k = (uint32_t)((g - groups) & 63);
+    const BloomSeg& sg = p.seg[t];
+    const uint64_t nb64 = 4 * (((sg.mask + 1) / 8 + 2) / 3);
+    if (k < 14) p.out[sg.json_out + k] = (uint8_t)kHead[k];
+    else if (k - 14 < sg.tail_len) p.out[sg.json_out + 14 + nb64 + (k - 14)] = sg.tail[k - 14];
+  }
+}
+
 }  // namespace
+
+hipError_t launch_bloom_tables(const BloomTables& p, uint64_t groups, hipStream_t s) {
+  if (p.nseg == 0) return hipSuccess;
+  const uint64_t keys = p.end - p.seg[0].first;
+  if (keys) {
+    hipLaunchKernelGGL(bloom_tables_build_kernel, dim3((unsigned)((keys + 255) / 256)), dim3(256),
+                       0, s, p);
+  }
+  const uint64_t threads = groups + 64ull * p.nseg;
+  hipLaunchKernelGGL(bloom_tables_json_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256),
+                     0, s, p, groups);
+  return hipGetLastError();
+}
 
 hipError_t launch_bloom_build(const BloomParams& p, hipStream_t s) {
   if (p.n == 0) return hipSuccess;

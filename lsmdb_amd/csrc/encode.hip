@@ -198,6 +198,25 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
 // the key / vs bytes of those entries.  The predicate grows with e, so each cut is a search:
 // one wave, 64 candidate counts per round trip.  A table ends at the first e >= 1 where it
 // holds, or takes every remaining entry.  Image size = data + 4 (blocks) + 4 (block count).
+// Finish's bloom tail for a table of cnt keys: JSONMarshal of bbloom.New(cnt, 0.01) + its BE32
+// length.  The float64 sizing follows Go's operation order (-1 * n * ln(w) / ln2^2, then
+// ceil(ln2 * size / n)) with the host's constants, so it rounds exactly like the host.
+__device__ __forceinline__ uint64_t bloom_tail_bytes(const CutParams& p, uint64_t cnt) {
+  const double n = (double)cnt;
+  const double size = -1 * n * p.logw / p.ln2sq;
+  const double locs = ceil(p.ln2 * size / n);
+  uint64_t entries = (uint64_t)size, bits = 1;
+  if (entries < 512) entries = 512;
+  while (bits < entries) bits <<= 1;
+  uint64_t l = (uint64_t)locs, digits = 1;
+  while (l >= 10) {
+    l /= 10;
+    digits++;
+  }
+  // {"FilterSet":"  base64   ","SetLocs":  digits  }   BE32
+  return 14 + 4 * ((bits / 8 + 2) / 3) + 12 + digits + 1 + 4;
+}
+
 __global__ void cut_tables_kernel(CutParams p) {
   const uint32_t lane = lane_id();
   uint64_t s = 0, blocks = 0, bytes = 0;
@@ -236,6 +255,7 @@ __global__ void cut_tables_kernel(CutParams p) {
       p.tbl_out[t] = bytes;
     }
     bytes += 10 * cnt + (kstart(s + cnt) - ks) + (vstart(s + cnt) - vs) + 13 * nb + 4 * nb + 4;
+    if (p.bloom) bytes += bloom_tail_bytes(p, cnt);
     blocks += nb;
     s += cnt;
     t++;

@@ -85,6 +85,10 @@ struct CutParams {
   uint64_t* tbl_out;    // tables_cap + 1
   uint32_t tables_cap;
   uint64_t* result;     // [0] tables, [1] blocks, [2] image bytes, [3] overflow
+  // bloom != 0: each image also reserves Finish's bloom tail (JSON + BE32 length,
+  // table/builder.go:189-195), sized by bbloom.New(cnt, 0.01) with host constants
+  uint32_t bloom;
+  double logw, ln2, ln2sq;  // ln(0.01), 0.69314718056, 0.69314718056^2 (Go's float64 values)
 };
 hipError_t launch_cut_tables(const CutParams& p, hipStream_t s);
 
@@ -169,14 +173,40 @@ struct BloomParams {
   uint32_t shift;           // 64 - log2(bits)
   uint32_t* flags;          // build: bit 0 = a key of <= 8 B
   uint8_t* has;             // probe: 1 = Has(key)
+  const uint32_t* key_base; // key 0 starts at *key_base (a sub-range of a stream), else 0
 };
 struct BloomJson {
   const uint64_t* bitset;
   uint64_t nbytes;          // bits / 8
   uint8_t* out;
   uint32_t head_len, tail_len;
-  uint8_t text[64];         // head ++ tail
+  uint8_t text[64];         // head ++ tail (++ BE32 of the JSON length: Finish's bloomLen)
 };
+// Finish's bloom tails of up to kBloomSegs compaction tables in one build + one JSON launch
+constexpr uint32_t kBloomSegs = 32;  // the segment table travels in the kernel arguments
+struct BloomSeg {
+  uint64_t word_off;   // the table's filter in the scratch (u64 words)
+  uint64_t mask;       // bits - 1
+  uint64_t json_out;   // byte offset of its JSON in out
+  uint64_t group_off;  // first base64 group of this table in the JSON launch
+  uint32_t first;      // first key (stream entry index)
+  uint32_t shift;      // 64 - log2(bits)
+  uint32_t locs;       // setLocs
+  uint32_t tail_len;   // tail text bytes incl. the BE32 length
+  uint8_t tail[28];    // ","SetLocs":N} ++ BE32(json length)
+};
+struct BloomTables {
+  const uint8_t* keys;
+  const uint32_t* key_end;
+  uint64_t* scratch;
+  uint8_t* out;
+  uint32_t* flags;
+  uint32_t nseg;
+  uint32_t end;        // one past the last key of the last table
+  BloomSeg seg[kBloomSegs];
+};
+static_assert(sizeof(BloomTables) + 8 <= 4096, "kernel arguments are limited to 4 KiB");
+hipError_t launch_bloom_tables(const BloomTables& p, uint64_t groups, hipStream_t s);
 hipError_t launch_bloom_build(const BloomParams& p, hipStream_t s);
 hipError_t launch_bloom_has(const BloomParams& p, hipStream_t s);
 hipError_t launch_bloom_json(const BloomJson& p, hipStream_t s);

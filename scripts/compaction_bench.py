@@ -107,13 +107,19 @@ def main():
 
     # output tables: ReachedCapacity(64 MiB) cut, then every table encoded in one launch
     mk, mke, mv, mve = m["key_data"], m["key_end"], m["val_data"], m["val_end"]
-    t_cut, cut = timed(torch, stream, lambda: codec.cut_tables_device(mke, mve, n_out, 64 << 20))
+    t_cut, cut = timed(torch, stream, lambda: codec.cut_tables_device(mke, mve, n_out, 64 << 20,
+                                                                      bloom=True))
     cr = cut["result"].cpu().numpy()
     ntab_out, out_bytes = int(cr[0]), int(cr[2])
+    cut["ntables"] = ntab_out
     d_out = torch.empty(out_bytes + 16, dtype=torch.uint8, device=dev)
     fl = torch.zeros(4, dtype=torch.int32, device=dev)
     t_enc, _ = timed(torch, stream, lambda: codec.encode_tables_device(
         cut, mk, mke, mv, mve, kb, vb, d_out, fl))
+    # Finish's bloom tails (complete .sst files); the host reads the cut's small arrays first
+    bfl = torch.zeros(1, dtype=torch.int32, device=dev)
+    codec.bloom_tables_device(cut, mk, mke, d_out, bfl)  # warm-up (and sizes the scratch)
+    t_bloom, _ = timed(torch, stream, lambda: codec.bloom_tables_device(cut, mk, mke, d_out, bfl))
 
     # oracle merge on the host, and the check
     import oracle_ffi
@@ -127,12 +133,15 @@ def main():
           np.array_equal(m["src"][:n_out].cpu().numpy().view(np.uint32), src))
     in_bytes = int(data.numel())
     print(json.dumps({
-        "what": "compaction replay: decode 1+%d C4 tables -> merge (2 runs) -> encode" % nbot,
+        "what": "compaction replay: decode 1+%d C4 tables -> merge (2 runs) -> encode + bloom "
+                "(complete .sst files)" % nbot,
         "input_table_bytes": in_bytes, "entries_in": n_in, "entries_out": n_out,
         "output_tables": ntab_out, "output_bytes": out_bytes,
         "decode_ms": round(t_dec, 4), "merge_ms": round(t_merge, 4), "cut_ms": round(t_cut, 4),
-        "encode_ms": round(t_enc, 4), "total_ms": round(t_dec + t_merge + t_cut + t_enc, 4),
-        "input_gibs": round(in_bytes / ((t_dec + t_merge + t_cut + t_enc) / 1e3) / (1 << 30), 2),
+        "encode_ms": round(t_enc, 4), "bloom_ms": round(t_bloom, 4),
+        "total_ms": round(t_dec + t_merge + t_cut + t_enc + t_bloom, 4),
+        "input_gibs": round(in_bytes / ((t_dec + t_merge + t_cut + t_enc + t_bloom) / 1e3) /
+                            (1 << 30), 2),
         "cpu_oracle_merge_ms": round(cpu_merge_s * 1e3, 1),
         "merge_matches_oracle": bool(ok)}))
     codec.close()

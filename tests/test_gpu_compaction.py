@@ -14,10 +14,13 @@ import open_cases as C
 pytestmark = pytest.mark.gpu
 
 
-def _oracle_tables(oracle, keys, vss, cap):
+def _oracle_tables(oracle, keys, vss, cap, bloom=False):
+    """The Go loop's tables: Finish minus bloom, or (bloom=True) the complete .sst bytes --
+    Finish's bbloom JSON over the table's keys (oracle/bbloom.c) + its BE32 length."""
     L = oracle.lib()
     out, i, n = [], 0, len(keys)
     while i < n:
+        i0 = i
         b = L.sstref_builder_new(100, 0)
         while i < n:
             if L.sstref_builder_reached_capacity(b, cap):
@@ -29,13 +32,20 @@ def _oracle_tables(oracle, keys, vss, cap):
         rs = ctypes.POINTER(ctypes.c_uint32)()
         ptr = L.sstref_builder_finish(b, ctypes.byref(ol), ctypes.byref(dl), ctypes.byref(rs),
                                       ctypes.byref(nr))
-        out.append(ctypes.string_at(ptr, ol.value))
+        img = ctypes.string_at(ptr, ol.value)
         L.sstref_builder_free(b)
+        if bloom:
+            kb, ke = oracle.columns(keys[i0:i], vss[i0:i])[:2]
+            bs, bits, locs, _ = oracle.bloom_build(kb, ke)
+            js = oracle.bloom_json(bs, bits, locs)
+            img += js + len(js).to_bytes(4, "big")
+        out.append(img)
     return out
 
 
-@pytest.mark.parametrize("cap", [1 << 20, 3 << 20])
-def test_device_compaction(codec, oracle, cap):
+@pytest.mark.parametrize("bloom", [False, True])
+@pytest.mark.parametrize("cap", [1 << 17, 1 << 20, 3 << 20])  # 1 << 17: > 32 tables
+def test_device_compaction(codec, oracle, cap, bloom):
     import torch
     from lsmdb_amd import workload
     parts = []
@@ -69,14 +79,16 @@ def test_device_compaction(codec, oracle, cap):
     r = m["result"].cpu().numpy()
     n_out, kb, vb = int(r[0]), int(r[1]), int(r[2])
     o = codec.compact_tables_device(m["key_data"], m["key_end"], m["val_data"], m["val_end"],
-                                    n_out, kb, vb, cap)
+                                    n_out, kb, vb, cap, bloom=bloom)
     codec.synchronize()
     assert int(o["flags"][0].item()) == 0
+    if bloom:
+        assert int(o["bloom_flags"][0].item()) == 0
     # oracle: merge order, then the Go Builder loop
     src = oracle.merge(kd, ke, rf)
     ks = [kd[(ke[i - 1] if i else 0): ke[i]] for i in src]
     vs = [vd[(ve[i - 1] if i else 0): ve[i]] for i in src]
-    ref = _oracle_tables(oracle, ks, vs, cap)
+    ref = _oracle_tables(oracle, ks, vs, cap, bloom)
     assert o["ntables"] == len(ref) and len(ref) >= 2
     img = o["out"].cpu().numpy().tobytes()
     tout = o["tbl_out"].cpu().numpy()
