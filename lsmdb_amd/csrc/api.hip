@@ -298,11 +298,15 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     // pure latency (C4 64 MiB, 5,163 blocks: 0.106 -> 0.071 ms) -- else one lane per block
     // (C2 1 GiB: lane 0.733 vs group 0.799 ms; C5 1 GiB, 185 blocks per CU whose shapes
     // rarely repeat: lane 1.02 vs group 1.08 ms with its give-up rule, 1.66 ms without).
-    // LSMGPU_WSC_WALK=lane / group / group2 / group4 / group16 / stream forces a walk.
+    // LSMGPU_WSC_WALK=lane / group / group2 / group4 / group16 / stream / scan forces a walk
+    // (scan: a verified data-parallel header scan, VALU-bound: C2 view 0.40 vs 0.31 ms).
     p.wwalk = nblk <= 64ull * (uint64_t)c->num_cus ? kWalkGroup : kWalkLane;
     p.wlanes = p.wwalk == kWalkGroup ? 8 : 1;
     if (wk_env && wk_env[0] == 'l') {
       p.wwalk = kWalkLane;
+      p.wlanes = 1;
+    } else if (wk_env && strncmp(wk_env, "scan", 4) == 0 && max_blk_len <= 4096) {
+      p.wwalk = kWalkScan;
       p.wlanes = 1;
     } else if (wk_env && wk_env[0] == 's' && max_blk_len <= 4096) {
       p.wwalk = kWalkStream;

@@ -16,6 +16,7 @@
 // Traffic: the input is read twice (walk touches every line; copy reads the bytes) -- the
 // price of taking the serial walk off the critical path.  Blocks must be < 64 KiB.
 #include <cstdlib>
+#include <type_traits>
 
 
 #include "codec_common.hpp"
@@ -127,6 +128,157 @@ __device__ __forceinline__ WalkResult walk_meta(const Src& src, const uint8_t* f
   return WalkResult{n, K, V, st};
 }
 
+// ---- scan walk (blocks <= 4 KiB): the header chain found by a data-parallel scan, not walked
+//
+// The serial chain pos -> pos + 10 + klen + vlen (iterator.go:93-135) is replaced by a test every
+// byte position can run on its own.  Every header Builder writes has plen == 0 (keyDiff returns
+// the whole key) and a back-pointer `prev` = the previous header's block offset
+// (builder.go:103-109; the terminator's prev is the last entry), which in a block < 64 KiB has
+// two zero high bytes -- except the first header's, 0xffffffff.  So a position q > 0 is a
+// CANDIDATE when bytes q, q+1, q+6, q+7 are zero (q = 0 when q, q+1 are), and it is ACCEPTED
+// when its successor end(q) = q + 10 + klen + vlen either closes the block (end == len; for
+// klen == 0, a terminator, only that) or holds a header whose prev == q.
+//
+// The test is only a filter; exactness comes from VERIFYING that the accepted positions, in
+// order, are the iterator's chain: the first is 0, each non-last one is an entry whose end is
+// the next, no terminator before the last, and the last ends at len.  Then the iterator,
+// started at 0, visits exactly these positions and stops after the last with status OK (every
+// entry has plen == 0, end <= len, and its header fits).  Any other block -- a false positive
+// (bytes inside a value that look like a chained header), plen > 0, an error status, no
+// terminator -- fails verification and takes the serial walk (walk_meta) from global memory.
+// Both produce the same records, so the copy kernel cannot tell them apart.
+//
+// Cost model (measured with SQ_INSTS_VALU): a wave64 VALU instruction holds a 16-lane SIMD for
+// 4 cycles, so a CU retires ~1 wave-instruction per cycle and HBM delivers a 4 KiB block per
+// ~420 CU cycles: the scan must stay well under ~400 wave-instructions per block.  Hence the
+// byte tests are OR-combined before one zero-byte test per dword, and flags are gathered in a
+// permuted bit order (2 instructions per dword); order is restored by the positional pass 2.
+constexpr uint32_t kNoPos = 0xffffffffu;
+
+// Candidate flags of a lane's 64-B LDS window, in PERMUTED order: bit 32m + 8j + k is window
+// position o = 32m + 4k + j (m < 2, k < 8, j < 4).  20 dwords: the window + 16 B of the next.
+__device__ __forceinline__ uint64_t header_candidates(const uint8_t* win) {
+  const uint4* w4 = reinterpret_cast<const uint4*>(win);
+  uint32_t w[20];
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const uint4 v = w4[i];
+    w[4 * i] = v.x;
+    w[4 * i + 1] = v.y;
+    w[4 * i + 2] = v.z;
+    w[4 * i + 3] = v.w;
+  }
+  uint32_t t[18];  // byte j of t[d]: window bytes 4d + j | 4d + j + 1
+#pragma unroll
+  for (int d = 0; d < 18; d++) t[d] = w[d] | __builtin_amdgcn_alignbyte(w[d + 1], w[d], 1);
+  uint32_t acc[2] = {0, 0};
+#pragma unroll
+  for (int d = 0; d < 16; d++) {
+    // byte j: bytes o, o+1, o+6, o+7 OR-ed (o = 4d + j); bit 7 of y's byte j set iff non-zero
+    const uint32_t v = t[d] | __builtin_amdgcn_alignbyte(t[d + 2], t[d + 1], 2);
+    const uint32_t y = ((v & 0x7f7f7f7fu) + 0x7f7f7f7fu) | v;
+    acc[d >> 3] = (acc[d >> 3] >> 1) | (y & 0x80808080u);  // dword 8m + k -> bits 8j + k
+  }
+  return ~(((uint64_t)acc[1] << 32) | acc[0]);  // zero flags
+}
+
+// klen (low 16) and vlen (high 16) of the header at LDS byte p
+__device__ __forceinline__ void scan_kv(const uint8_t* slot, uint32_t p, uint32_t& klen,
+                                        uint32_t& vlen) {
+  const uint32_t x = lds_u32(slot, p + 2);
+  klen = __builtin_amdgcn_perm(0u, x, 0x0c0c0001u);
+  vlen = __builtin_amdgcn_perm(0u, x, 0x0c0c0203u);
+}
+
+// One block in the wave's LDS slot (byte 0 at slot + sh, len <= 4096; the slot holds 4128 B).
+// Writes the same records as walk_meta; the result is valid in lane 0.
+__device__ WalkResult scan_block(const uint8_t* slot, uint32_t sh, uint32_t len,
+                                 const uint8_t* gblk, uint2* meta, uint32_t lane) {
+  const int base = 64 * (int)lane - (int)sh;  // block position of the lane's window byte 0
+  // pass 1 (any order): accept candidates; per lane: positional mask, count / key / value sums,
+  // the lowest accepted position and the end of the highest, the terminator (if any)
+  uint64_t cand = len >= 10 ? header_candidates(slot + 64 * lane) : 0ull;
+  uint64_t acc = 0;
+  uint32_t c = 0, Ks = 0, Vs = 0, lo_q = kNoPos, hi_q = 0, hi_end = kNoPos, tq = kNoPos;
+  auto accept = [&](uint32_t q, uint32_t o) {
+    uint32_t klen, vlen;
+    scan_kv(slot, sh + q, klen, vlen);
+    const uint32_t end = q + 10 + klen + vlen;
+    const bool succ = end + 10 <= len;  // a successor header fits: its prev must point back
+    const uint32_t prev = bswap32(lds_u32(slot, sh + (succ ? end + 6 : 0u)));  // (clamped read)
+    // a terminator (finishBlock) closing the block; the block's last entry (no terminator); an
+    // entry whose successor's prev points back
+    const bool a = klen == 0 ? end == len : (end == len || (succ && prev == q));
+    if (!a) return;
+    acc |= 1ull << o;
+    lo_q = min(lo_q, q);
+    if (hi_end == kNoPos || q > hi_q) {
+      hi_q = q;
+      hi_end = end;
+    }
+    if (klen == 0) {
+      tq = q;
+    } else {
+      c++;
+      Ks += klen;
+      Vs += vlen;
+    }
+  };
+  if (lane == 0 && len >= 10 && (lds_u32(slot, sh) & 0xffffu) == 0) accept(0, sh);  // q = 0
+  while (cand) {
+    const uint32_t bit = (uint32_t)__builtin_ctzll(cand);
+    cand &= cand - 1;
+    const uint32_t o = (bit & 32u) + 4 * (bit & 7u) + ((bit >> 3) & 3u);
+    const int qi = base + (int)o;
+    if (qi <= 0 || (uint32_t)qi + 10 > len) continue;  // outside the block (q = 0: above)
+    accept((uint32_t)qi, o);
+  }
+  // entries (<= 409) and key bytes (<= 4096) share one scan: c | Ks << 16 cannot carry over
+  const uint32_t ick = wave_scan_sat(c | (Ks << 16), lane), iv = wave_scan_sat(Vs, lane);
+  const uint32_t ic = ick & 0xffffu, ik = ick >> 16;
+  const uint32_t n = readlane(ic, 63), K = readlane(ik, 63), V = readlane(iv, 63);
+  // pass 2 (positional): the lane's records, and its chain -- each accepted position is the
+  // previous one's end, nothing after a terminator
+  uint32_t idx = ic - c, kr = ik - Ks, vr = iv - Vs, last_end = kNoPos;
+  bool ok = true;
+  for (uint64_t a = acc; a;) {
+    const uint32_t o = (uint32_t)__builtin_ctzll(a);
+    a &= a - 1;
+    const uint32_t q = (uint32_t)(base + (int)o);
+    uint32_t klen, vlen;
+    scan_kv(slot, sh + q, klen, vlen);
+    ok = ok && (last_end == kNoPos || last_end == q);
+    if (klen == 0) {  // the terminator: the lane's last accepted position
+      ok = ok && a == 0;
+      break;
+    }
+    last_end = q + 10 + klen + vlen;
+    meta[idx] = make_uint2(q | (vr << 16), kr);
+    kr += klen;
+    vr += vlen;
+    idx++;
+  }
+  // across lanes: each non-empty lane's last end is the next non-empty lane's first position
+  // (len for the last one); the lowest non-empty lane starts at 0
+  const bool ne = acc != 0;
+  const uint64_t neb = __ballot(ne);
+  const uint64_t later = lane == 63 ? 0ull : neb >> (lane + 1);
+  const uint32_t nl = later ? lane + 1 + (uint32_t)__builtin_ctzll(later) : lane;
+  const uint32_t nextf = (uint32_t)__shfl((int)lo_q, (int)nl);
+  const bool bad = ne && (!ok || hi_end != (later ? nextf : len));
+  const bool good = neb != 0 && __ballot(bad) == 0 && readlane(lo_q, 0) == 0;
+  if (!good) {  // serial walk: every stop rule in the iterator's order (rewrites every record)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // pass 2's stores land first
+    WalkResult r{0, 0, 0, LSMGPU_BLK_OK};
+    if (lane == 0) r = walk_meta(GlobalSrc{gblk}, nullptr, len, meta);
+    return r;
+  }
+  const uint64_t tb = __ballot(tq != kNoPos);
+  const uint32_t stop = tb ? readlane(tq, (uint32_t)__builtin_ctzll(tb)) : len;
+  if (lane == 0) meta[n] = make_uint2(stop | (V << 16), K);  // sentinel
+  return WalkResult{n, K, V, LSMGPU_BLK_OK};
+}
+
 // K1: lane = block; a workgroup = a tile of 256 consecutive blocks, tiles taken in ticket order
 // (p.gcnt[0]).  After the walk the workgroup scans its blocks' {entries, key bytes, value
 // bytes}, publishes the tile aggregate and finds the tile's output base by decoupled look-back
@@ -147,10 +299,13 @@ template <int MODE, uint32_t TB>  // TB = blocks per tile (<= 256 threads: threa
 __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   static_assert(TB <= 256, "one thread per block of the tile");
   constexpr bool STREAM = MODE == kWalkStream;
+  constexpr bool SCAN = MODE == kWalkScan;
   constexpr uint32_t kStageBytes = 256 * kWalkStage * sizeof(uint2);
-  // group walk: a 32-record ring per block (its LDS also serves the view epilogue's owner map)
+  // group walk: a 32-record ring per block (its LDS also serves the view epilogue's owner map);
+  // scan walk: one block slot per wave
   constexpr uint32_t kLdsBytes = STREAM ? kSwSub * kSwSlot
-                                        : MODE == kWalkGroup ? TB * 16 * sizeof(uint2) : kStageBytes;
+                                 : SCAN ? 4 * kSwSlot
+                                 : MODE == kWalkGroup ? TB * 16 * sizeof(uint2) : kStageBytes;
   static_assert(MODE != kWalkLane || kLdsBytes == kStageBytes,
                 "the lane walk stages 16 records per lane");
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
@@ -159,9 +314,9 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   __shared__ uint32_t s_wave[4][3];
   __shared__ uint32_t s_ex[3];
   __shared__ uint32_t s_first[257];  // p.wfuse: tile-relative first entry of each block
-  __shared__ uint32_t s_off[MODE == kWalkGroup ? TB : 256];  // each block's input offset
-  __shared__ uint32_t s_len[STREAM ? 256 : 1];
-  constexpr uint32_t kRes = MODE == kWalkLane ? 1 : MODE == kWalkGroup ? TB : 256;
+  __shared__ uint32_t s_off[MODE == kWalkGroup || SCAN ? TB : 256];  // each block's input offset
+  __shared__ uint32_t s_len[STREAM ? 256 : SCAN ? TB : 1];
+  constexpr uint32_t kRes = MODE == kWalkLane ? 1 : MODE == kWalkGroup || SCAN ? TB : 256;
   __shared__ uint32_t s_res[4][kRes];  // stream / group walk: n, K, V, status per block
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t ntiles = (p.nblk + TB - 1) / TB;
@@ -345,6 +500,88 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
       t[2] = V;
       p.wstatus[b] = st;
     }
+  } else if constexpr (SCAN) {
+    // wave w takes the tile's blocks [w * TB / 4, (w + 1) * TB / 4) one after another: block i's
+    // 16-B aligned lines go into the wave's LDS slot (coalesced, 1 KiB per wave instruction),
+    // block i + 1's loads are issued into registers, then block i is scanned (scan_block)
+    constexpr uint32_t PW = TB / 4;
+    static_assert(TB % 4 == 0, "four waves share the tile");
+    if (b < p.nblk) {
+      s_off[tid] = p.blk_off[b];
+      s_len[tid] = p.blk_len[b];
+    }
+    __syncthreads();
+    static_assert(PW <= 64, "a wave's blocks: one [off, len) per lane");
+    const uint32_t nb = min(TB, p.nblk - tile * TB);
+    const uint32_t i0 = wave * PW, i1 = min(i0 + PW, nb);
+    uint8_t* const slot = lds + wave * kSwSlot;
+    // lane i holds block i0 + i's [off, len): a block's values are one v_readlane away
+    const uint32_t w_off = i0 + lane < i1 ? s_off[i0 + lane] : 0u;
+    const uint32_t w_len = i0 + lane < i1 ? s_len[i0 + lane] : 0u;
+    // two blocks' loads in flight while a third is scanned (one in flight left the wave
+    // waiting on HBM latency after every block)
+    uint4 R0[4], R1[4], RT0 = make_uint4(0, 0, 0, 0), RT1 = make_uint4(0, 0, 0, 0);
+    auto issue = [&](uint32_t bi, uint4 (&R)[4], uint4& RT) {
+      const uint32_t off = readlane(w_off, bi - i0), len = readlane(w_len, bi - i0);
+      const uint64_t a0 = off & ~15ull;
+      if (len <= kSwMaxLen && a0 + kSwSlot <= p.data_len) {  // uniform: no per-chunk checks
+        const uint4* src = reinterpret_cast<const uint4*>(p.data + a0);
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) R[i] = src[lane + 64 * i];
+        if (lane < 2) RT = src[256 + lane];
+      } else {  // the buffer's last lines (or an oversize block: zeros)
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) R[i] = sw_chunk(p, off, len, lane + 64 * i);
+        if (lane < 2) RT = sw_chunk(p, off, len, 256 + lane);
+      }
+    };
+    auto scan_one = [&](uint32_t bi, uint4 (&R)[4], uint4& RT) {
+      wave_lds_fence();  // the previous block's reads are done with the slot
+#pragma unroll
+      for (uint32_t i = 0; i < 4; i++) *reinterpret_cast<uint4*>(slot + 16 * (lane + 64 * i)) = R[i];
+      if (lane < 2) *reinterpret_cast<uint4*>(slot + 16 * (256 + lane)) = RT;
+      wave_lds_fence();
+      if (bi + 2 < i1) issue(bi + 2, R, RT);  // in flight while blocks bi, bi + 1 are scanned
+      const uint32_t off = readlane(w_off, bi - i0), len = readlane(w_len, bi - i0);
+      uint2* meta = reinterpret_cast<uint2*>(p.wmeta) + (uint64_t)(tile * TB + bi) * p.wcap;
+      WalkResult r{0, 0, 0, LSMGPU_BLK_RANGE};
+      if ((uint64_t)off + len > p.data_len) {
+        if (lane == 0) meta[0] = make_uint2(0, 0);
+      } else if (len > kSwMaxLen) {  // only if the caller's max_blk_len was wrong: global walk
+        if (lane == 0) r = walk_meta(GlobalSrc{p.data + off}, nullptr, len, meta);
+      } else if (p.ablate & 4) {  // timing only: loads, no scan
+        r = WalkResult{0, 0, 0, LSMGPU_BLK_OK};
+        if (lane == 0) meta[0] = make_uint2(0, 0);
+      } else {
+        r = scan_block(slot, off & 15u, len, p.data + off, meta, lane);
+      }
+      if (lane == 0) {
+        s_res[0][bi] = r.n;
+        s_res[1][bi] = r.K;
+        s_res[2][bi] = r.V;
+        s_res[3][bi] = r.status;
+      }
+    };
+    if (i0 < i1) issue(i0, R0, RT0);
+    if (i0 + 1 < i1) issue(i0 + 1, R1, RT1);
+    for (uint32_t bi = i0; bi < i1; bi += 2) {
+      scan_one(bi, R0, RT0);
+      if (bi + 1 < i1) scan_one(bi + 1, R1, RT1);
+    }
+    // the records are global stores of every wave: complete before the epilogue reads them
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (b < p.nblk) {
+      n = s_res[0][tid];
+      K = s_res[1][tid];
+      V = s_res[2][tid];
+      st = s_res[3][tid];
+      uint64_t* t = p.wstat + 3ull * b;
+      t[0] = n;
+      t[1] = K;
+      t[2] = V;
+      p.wstatus[b] = st;
+    }
   } else if (b < p.nblk) {
     uint2* row = stage + tid * kWalkStage;
     const uint32_t off = p.blk_off[b], len = p.blk_len[b];
@@ -460,13 +697,14 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   const uint64_t e0 = s_ex[0];
   // entry -> block map in the walk's staging rows (free now): each thread marks its block's
   // entries, so the lookup is one LDS read (tiles of more entries: binary search)
-  uint16_t* owner = reinterpret_cast<uint16_t*>(stage);
-  // a u16 owner slot names one of the tile's 256 blocks
-  static_assert(256 <= 65536, "tile width must fit the u16 owner slot");
-  const bool mapped = nt <= kLdsBytes / sizeof(uint16_t);  // u16 slots in the walk's LDS
+  // (u8 slots for the scan walk, whose LDS is smaller: 256 blocks still fit a byte)
+  using Owner = typename std::conditional<SCAN, uint8_t, uint16_t>::type;
+  Owner* owner = reinterpret_cast<Owner*>(stage);
+  static_assert(TB - 1 <= (uint32_t)(Owner)~Owner(0), "tile width must fit the owner slot");
+  const bool mapped = nt <= kLdsBytes / sizeof(Owner);  // owner slots in the walk's LDS
   if (mapped) {
     const uint32_t f = s_first[tid];
-    for (uint32_t i = 0; i < n; i++) owner[f + i] = (uint16_t)tid;
+    for (uint32_t i = 0; i < n; i++) owner[f + i] = (Owner)tid;
     __syncthreads();
   }
   for (uint32_t e = tid; e < nt; e += 256) {
@@ -931,7 +1169,9 @@ hipError_t launch_decode_tile(const DecodeParams& p, hipStream_t s) {
 
 hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s) {
   const uint32_t nblk = p.nblk;
-  if (p.wwalk == kWalkStream)
+  if (p.wwalk == kWalkScan)
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkScan, 256>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
+  else if (p.wwalk == kWalkStream)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkStream, kSwTile>), dim3((nblk + kSwTile - 1) / kSwTile),
                        dim3(256), 0, s, p);
   else if (p.wwalk == kWalkGroup && p.wlanes == 2)

@@ -47,6 +47,7 @@ struct DecodeParams {
   uint32_t wfuse;           // walk-scan-copy, view-only mode: the walk writes the view index
                             // and per-block outputs itself (no copy launch)
   uint32_t wwalk;           // walk-scan-copy walk: kWalkLane / kWalkStream / kWalkGroup (+ lanes)
+                            // / kWalkScan
   uint32_t wlanes;          // kWalkGroup: lanes per block (4, 8 or 16)
 };
 
@@ -215,6 +216,7 @@ hipError_t launch_bloom_json(const BloomJson& p, hipStream_t s);
 constexpr int kWalkLane = 0;    // one lane per block, header by header from HBM
 constexpr int kWalkStream = 1;  // blocks <= 4 KiB through LDS, walked there
 constexpr int kWalkGroup = 2;   // wlanes lanes per block, speculative same-shape runs from HBM
+constexpr int kWalkScan = 3;    // blocks <= 4 KiB: a wave per block, data-parallel header scan
 constexpr uint32_t kFscRec = 412;  // 409 entries of >= 10 B in 4096 B + the sentinel, rounded
 hipError_t launch_decode_fsc(const DecodeParams& p, int num_cus, hipStream_t s);
 // which decode path a batch takes: 0 register-lag (<= 4 KiB), 1 LDS-lag, 2 walk-scan-copy

@@ -1,5 +1,6 @@
 """Per-kernel mean of every PMC counter in rocprofv3 counter_collection CSVs."""
 import csv
+import os
 import sys
 from collections import defaultdict
 
@@ -11,7 +12,7 @@ for path in sys.argv[1:]:
         agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[k].add(r["Dispatch_Id"])
     for k, v in agg.items():
-        if "decode" not in k:
+        if os.environ.get("PMC_FILTER", "decode") not in k:
             continue
         n = len(disp[k])
         print(path, k, "dispatches", n)

@@ -499,11 +499,12 @@ def test_wsc_lanes_per_entry(codec, oracle, monkeypatch, lanes):
     _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln), f"J={lanes}")
 
 
-@pytest.mark.parametrize("walk", ["stream", "lane", "group", "group2", "group4", "group16"])
+@pytest.mark.parametrize("walk", ["scan", "stream", "lane", "group", "group2", "group4", "group16"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
-    """Walk-scan-copy's walks (LSMGPU_WSC_WALK): blocks <= 4 KiB streamed through LDS, one lane
-    per block from HBM, or 8 / 4 / 16 lanes per block guessing same-shape runs from HBM.  C2 /
+    """Walk-scan-copy's walks (LSMGPU_WSC_WALK): blocks <= 4 KiB scanned for their headers by a
+    wave in LDS, or streamed through LDS and walked there, one lane per block from HBM, or 8 / 4
+    / 16 lanes per block guessing same-shape runs from HBM.  C2 /
     C3 blocks, short and tiny entries (> 64 per block), every KAT block (error statuses,
     terminators, plen > 0) at odd alignments, prefix-compressed random blocks, a ragged last
     tile and a block ending at the buffer's end (plus C5 32 KiB blocks for the HBM walks)."""
@@ -517,7 +518,7 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
              oracle.build_cols(c3.keys, c3.key_end, c3.vs, c3.vs_end, 0, 4096)[0],
              oracle.build_cols(*_random_cols(20000, 25), 0, 4096)[0],
              oracle.build_cols(*_random_cols(60000, 26, 9, 10, 3, 4), 0, 4096)[0]]
-    if walk != "stream":
+    if walk not in ("stream", "scan"):  # LDS walks take blocks <= 4 KiB
         c5 = _cols(5, 6000, seed=27)
         parts.append(oracle.build_cols(c5.keys, c5.key_end, c5.vs, c5.vs_end, 0,
                                        c5.block_bytes)[0])
@@ -581,3 +582,76 @@ def test_wsc_mixed_copy(codec, oracle, monkeypatch):
     for sl in (slice(None), slice(None, None, -1), slice(3, None, 7)):
         oo, ll = np.ascontiguousarray(o2[sl]), np.ascontiguousarray(l2[sl])
         _assert_same(codec.decode_host(kd, oo, ll), oracle.decode(kd, oo, ll), f"{sl}")
+
+
+def _block_entries(block):
+    """(pos, klen, vlen) of a plen == 0 block's entries, walked as iterator.go:93-135 does."""
+    out, pos = [], 0
+    while pos + 10 <= len(block):
+        plen, klen, vlen = (int.from_bytes(block[pos + i:pos + i + 2], "big") for i in (0, 2, 4))
+        if plen or klen == 0 or pos + 10 + klen + vlen > len(block):
+            break
+        out.append((pos, klen, vlen))
+        pos += 10 + klen + vlen
+    return out
+
+
+@pytest.mark.parametrize("mode", ["materialize", "view"])
+def test_scan_walk_adversarial(codec, oracle, monkeypatch, mode):
+    """The scan walk's header test is a filter; these blocks defeat it.  Keys and values over
+    the bytes {0, 1, 2, 3} (zero pairs everywhere, back-pointers that sometimes match), zero
+    values, fake chained headers planted inside values (a candidate whose successor's prev
+    points back at it: accepted, so verification must send the block to the serial walk), fake
+    terminators, and blocks cut short (no terminator, a torn terminator, torn entries).  Every
+    block must decode exactly as the oracle's iterator does."""
+    from lsmdb_amd.codec import MODE_MATERIALIZE, MODE_VIEW
+    monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
+    monkeypatch.setenv("LSMGPU_WSC_WALK", "scan")
+    monkeypatch.setenv("LSMGPU_WSC_VIEWFUSE", "1")
+    rng = np.random.default_rng(77)
+    parts = []
+    for seed in range(4):
+        keys, ke, vs, ve = _random_cols(6000, 100 + seed, 9, 24, 0, 40)
+        keys[:] = rng.integers(0, 4, keys.size)
+        vs[:] = rng.integers(0, 4, vs.size)
+        parts.append(oracle.build_cols(keys, ke, vs, ve, 0, 4096)[0])
+    keys, ke, vs, ve = _random_cols(8000, 200, 9, 30, 3, 90)
+    vs[:] = 0
+    parts.append(oracle.build_cols(keys, ke, vs, ve, 0, 4096)[0])
+    c2 = _cols(2, 30000, seed=201)
+    parts.append(oracle.build_cols(c2.keys, c2.key_end, c2.vs, c2.vs_end, 0, 4096)[0])
+    data, off, ln = _sst_blocks(oracle, parts)
+    kd = bytearray(data)
+    offs, lens = [int(x) for x in off], [int(x) for x in ln]
+    planted = 0
+    for b in range(len(offs)):
+        o, n = offs[b], lens[b]
+        ents = _block_entries(bytes(kd[o:o + n]))
+        kind = b % 4
+        for pos, klen, vlen in ents:
+            vstart = pos + 10 + klen
+            if kind == 0 and vlen >= 24:  # fake entry at p (klen 1, vlen 0) + successor prev = p
+                p = vstart + int(rng.integers(0, vlen - 23))
+                kd[o + p:o + p + 6] = bytes([0, 0, 0, 1, 0, 0])
+                kd[o + p + 11 + 6:o + p + 11 + 10] = p.to_bytes(4, "big")
+                planted += 1
+            elif kind == 1 and vlen >= 13:  # a fake terminator inside a value
+                p = vstart + int(rng.integers(0, vlen - 12))
+                kd[o + p:o + p + 6] = bytes([0, 0, 0, 0, 0, 3])
+        if kind == 2 and ents:  # cut: no terminator / torn terminator / torn last entry
+            cut = [13, 1, 5, 20][(b // 4) % 4]
+            lens[b] = max(0, n - cut)
+    assert planted > 100
+    kd = bytes(kd)
+    o2, l2 = np.array(offs, np.uint32), np.array(lens, np.uint32)
+    m = MODE_MATERIALIZE | MODE_VIEW if mode == "materialize" else MODE_VIEW
+    for sl in (slice(None), slice(None, None, -1)):
+        oo, ll = np.ascontiguousarray(o2[sl]), np.ascontiguousarray(l2[sl])
+        g = codec.decode_host(kd, oo, ll, mode=m)
+        o = oracle.decode(kd, oo, ll)
+        if mode == "materialize":
+            _assert_same(g, o, f"adversarial {sl}")
+        else:
+            assert g.n_entries == o.n_entries and np.array_equal(g.view, o.view)
+            assert np.array_equal(g.blk_first, o.blk_first)
+            assert np.array_equal(g.blk_status, o.blk_status)
