@@ -692,7 +692,7 @@ int lsmgpu_merge_runs_async(lsmgpu_ctx* c, const lsmgpu_runs* in, const lsmgpu_m
   }
   // emit tile records share the decode's look-back scratch (epoch-tagged, stream-ordered):
   // [ticket u32, padded to 256 B][64 B per tile]
-  const size_t lb_need = 256 + ((size_t)n / kMergeEmitTile + 1) * 64;
+  const size_t lb_need = 256 + ((size_t)n / 256 + 1) * 64;  // emit tiles of >= 256 positions
   if (lb_need > c->lb.cap) {
     HIPC(hipStreamSynchronize(c->stream));
     HIPC(c->lb.ensure(lb_need));

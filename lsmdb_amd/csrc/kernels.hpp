@@ -147,7 +147,7 @@ struct MergeParams {
   uint64_t ent_cap;
   uint64_t* result;
 };
-constexpr uint32_t kMergeEmitTile = 1024;  // merged positions per emit workgroup
+constexpr uint32_t kMergeEmitTile = 1024;  // merged positions per emit workgroup (the largest tile)
 hipError_t launch_merge(const MergeParams& p, hipStream_t s);
 
 // launchers (return hipError_t)

@@ -21,6 +21,8 @@
 //                           per kept entry copy 16-B pieces of key and raw vs-enc bytes
 // Unsorted runs (the heap would interleave them differently) and keys <= 8 B are reported in
 // result[3] and produce no output.
+#include <cstdlib>
+
 #include "decode_common.hpp"
 #include "kernels.hpp"
 
@@ -134,7 +136,6 @@ __global__ void merge_rank_kernel(MergeParams p) {
 // over the tile records (epoch-tagged granules in p.lb, as in the decode walk), writes the
 // end offsets and source index of its kept entries, then 8 lanes per kept entry copy the key
 // and raw vs-enc bytes as 16-B pieces.  No permutation-sized scratch beyond dst.
-constexpr uint32_t kEmitTile = kMergeEmitTile;
 
 __device__ __forceinline__ uint4 load16u(const uint8_t* p) {  // any alignment
   uint4 v;
@@ -143,7 +144,13 @@ __device__ __forceinline__ uint4 load16u(const uint8_t* p) {  // any alignment
 }
 __device__ __forceinline__ void store16u(uint8_t* p, uint4 v) { __builtin_memcpy(p, &v, 16); }
 
+// PP merged positions per thread (a tile is 256 * PP positions); G entries per 8-lane group
+// per gather trip, every first piece loaded before any is stored
+template <uint32_t PP, uint32_t G>
 __global__ void __launch_bounds__(256) merge_emit_kernel(MergeParams p) {
+  constexpr uint32_t kEmitTile = 256 * PP;
+  // the look-back scratch holds one record per 256 positions (lsmgpu_merge_runs_async)
+  static_assert(kEmitTile >= 256 && kEmitTile <= kMergeEmitTile, "emit tile size");
   __shared__ uint4 s_ent[kEmitTile][2];  // kept entries: {i, ks, kl, bk}, {vs, vl, bv, bn}
   __shared__ uint32_t s_tile;
   __shared__ uint32_t s_wave[4][3];
@@ -158,20 +165,20 @@ __global__ void __launch_bounds__(256) merge_emit_kernel(MergeParams p) {
   }
   __syncthreads();
   const uint32_t tile = s_tile;
-  const uint32_t q0 = tile * kEmitTile + 4 * tid;
-  uint32_t src[4], kl[4], vl[4], ks[4], vs[4];
+  const uint32_t q0 = tile * kEmitTile + PP * tid;
+  uint32_t src[PP], kl[PP], vl[PP], ks[PP], vs[PP];
   uint32_t keepm = 0, tn = 0, tk = 0, tv = 0;
   if (q0 < p.n) {
-    if (q0 + 4 <= p.n) {
-      const uint4 d = *reinterpret_cast<const uint4*>(p.dst + q0);
-      src[0] = d.x; src[1] = d.y; src[2] = d.z; src[3] = d.w;
+    if (q0 + PP <= p.n) {
+#pragma unroll
+      for (uint32_t c = 0; c < PP; c++) src[c] = p.dst[q0 + c];
     } else {
-      for (uint32_t c = 0; c < 4; c++) src[c] = q0 + c < p.n ? p.dst[q0 + c] : 0u;
+      for (uint32_t c = 0; c < PP; c++) src[c] = q0 + c < p.n ? p.dst[q0 + c] : 0u;
     }
     uint32_t lp = 0;
     const uint8_t* kp = nullptr;
     if (q0 > 0) kp = key_of(p, p.dst[q0 - 1], lp);
-    for (uint32_t c = 0; c < 4; c++) {
+    for (uint32_t c = 0; c < PP; c++) {
       if (q0 + c >= p.n) { kl[c] = vl[c] = ks[c] = vs[c] = 0; continue; }
       const uint32_t i = src[c];
       ks[c] = i ? p.ke[i - 1] : 0u;
@@ -239,7 +246,7 @@ __global__ void __launch_bounds__(256) merge_emit_kernel(MergeParams p) {
   bk += s_ex[1];
   bv += s_ex[2];
   const uint32_t n0 = s_ex[0];
-  for (uint32_t c = 0; c < 4; c++) {
+  for (uint32_t c = 0; c < PP; c++) {
     if (!((keepm >> c) & 1u)) continue;
     const uint32_t bn = n0 + ln;
     s_ent[ln][0] = make_uint4(src[c], ks[c], kl[c], bk);
@@ -256,9 +263,9 @@ __global__ void __launch_bounds__(256) merge_emit_kernel(MergeParams p) {
     bv += vl[c];
   }
   __syncthreads();
-  // gather: 8 lanes per kept entry, kGatherG entries per lane per trip with every first-round
+  // gather: 8 lanes per kept entry, G entries per lane per trip with every first-round
   // 16-B piece loaded before any is stored (more loads in flight per wave)
-  constexpr uint32_t kGatherG = 4;
+  constexpr uint32_t kGatherG = G;
   const uint32_t m = s_wave[0][0] + s_wave[1][0] + s_wave[2][0] + s_wave[3][0];
   const uint32_t sub = tid & 7u;
   for (uint32_t e0 = tid >> 3; e0 < m; e0 += kGatherG * (256 / 8)) {
@@ -315,8 +322,19 @@ hipError_t launch_merge(const MergeParams& p, hipStream_t s) {
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(merge_rank_kernel, g, dim3(256), 0, s, p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(merge_emit_kernel, dim3((p.n + kEmitTile - 1) / kEmitTile), dim3(256), 0,
-                       s, p);
+    // positions per thread (tile = 256 x PP); LSMGPU_MERGE_PP=1|2|4 forces it (A/B)
+    const int pp_env = getenv("LSMGPU_MERGE_PP") ? atoi(getenv("LSMGPU_MERGE_PP")) : 0;
+    const int pp = pp_env == 1 || pp_env == 2 || pp_env == 4 ? pp_env : 4;
+    // gather depth: LSMGPU_MERGE_G=8 keeps 8 first pieces in flight per lane (A/B), default 4
+    const bool g8 = getenv("LSMGPU_MERGE_G") && atoi(getenv("LSMGPU_MERGE_G")) == 8;
+    if (pp == 1)
+      hipLaunchKernelGGL((merge_emit_kernel<1, 4>), dim3((p.n + 255) / 256), dim3(256), 0, s, p);
+    else if (pp == 2)
+      hipLaunchKernelGGL((merge_emit_kernel<2, 4>), dim3((p.n + 511) / 512), dim3(256), 0, s, p);
+    else if (g8)
+      hipLaunchKernelGGL((merge_emit_kernel<4, 8>), dim3((p.n + 1023) / 1024), dim3(256), 0, s, p);
+    else
+      hipLaunchKernelGGL((merge_emit_kernel<4, 4>), dim3((p.n + 1023) / 1024), dim3(256), 0, s, p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   hipLaunchKernelGGL(merge_flags_kernel, dim3(1), dim3(64), 0, s, p);

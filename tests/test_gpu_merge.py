@@ -110,3 +110,16 @@ def test_merge_compaction_replay(codec, oracle):
     assert len(src) < int(run_first[-1])          # duplicates were dropped
     assert np.array_equal(gsrc, src)
     assert gk == ek and gv == ev
+
+
+@pytest.mark.parametrize("knob,val", [("LSMGPU_MERGE_PP", "1"), ("LSMGPU_MERGE_PP", "2"),
+                                      ("LSMGPU_MERGE_G", "8")])
+def test_merge_emit_instances(codec, oracle, monkeypatch, knob, val):
+    """Every merge_emit_kernel<PP, G> instance the A/B knobs select (tiles of 256 / 512
+    positions, 8 gather pieces in flight): duplicates across and inside runs, several tiles,
+    a ragged last tile, bit-exact against the oracle MergeIterator."""
+    monkeypatch.setenv(knob, val)
+    rng = np.random.default_rng(int(val) + len(knob))
+    users = [b"u%04d" % i for i in range(900)] + [b"u01", b"u0", b"u0100"]
+    runs = [_run(rng, 1500, users, 9), _run(rng, 1300, users, 9), _run(rng, 700, users, 9)]
+    _check(codec, oracle, runs, f"{knob}={val}")
