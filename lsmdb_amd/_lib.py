@@ -44,6 +44,8 @@ EXPORTED_SYMBOLS = (
     "lsmgpu_set_stream",
     "lsmgpu_get_stream",
     "lsmgpu_synchronize",
+    "lsmgpu_set_kernel_timing",
+    "lsmgpu_kernel_times",
     "lsmgpu_strerror",
     "lsmgpu_abi_version",
     "lsmgpu_parse_index",
@@ -153,6 +155,11 @@ def _load() -> ctypes.CDLL:
     lib.lsmgpu_get_stream.restype = c_void_p
     lib.lsmgpu_synchronize.argtypes = [c_void_p]
     lib.lsmgpu_synchronize.restype = c_int
+    lib.lsmgpu_set_kernel_timing.argtypes = [c_void_p, c_int]
+    lib.lsmgpu_set_kernel_timing.restype = c_int
+    lib.lsmgpu_kernel_times.argtypes = [c_void_p, ctypes.POINTER(ctypes.c_float),
+                                        ctypes.POINTER(ctypes.c_float)]
+    lib.lsmgpu_kernel_times.restype = c_int
     lib.lsmgpu_strerror.argtypes = [c_int]
     lib.lsmgpu_strerror.restype = ctypes.c_char_p
     lib.lsmgpu_abi_version.argtypes = []

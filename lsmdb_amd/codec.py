@@ -156,6 +156,18 @@ class Codec:
     def synchronize(self) -> None:
         check(lib().lsmgpu_synchronize(self._ctx), "synchronize")
 
+    # -- diagnostics: per-kernel HIP-event timing of walk-scan-copy decodes
+    def set_kernel_timing(self, on: bool) -> None:
+        check(lib().lsmgpu_set_kernel_timing(self._ctx, 1 if on else 0), "set_kernel_timing")
+
+    def kernel_times(self) -> tuple:
+        """(walk ms, copy ms) of the last timed walk-scan-copy decode (waits for it)."""
+        import ctypes
+        w, c = ctypes.c_float(), ctypes.c_float()
+        check(lib().lsmgpu_kernel_times(self._ctx, ctypes.byref(w), ctypes.byref(c)),
+              "kernel_times")
+        return float(w.value), float(c.value)
+
     # -- decode, host buffers (table.Table path)
     def decode_host(self, data, blk_off: np.ndarray, blk_len: np.ndarray,
                     mode: int = MODE_MATERIALIZE | MODE_VIEW) -> HostDecoded:

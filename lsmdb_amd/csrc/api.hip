@@ -64,6 +64,10 @@ struct lsmgpu_ctx {
   DevBuf merge_tmp;      // k-way merge: permutation, flags, tile bases, splitters
   // staging for host-memory calls
   DevBuf s_data, s_off, s_len, s_kd, s_ke, s_vd, s_ve, s_view, s_bf, s_bs, s_a, s_b, s_c, s_d;
+  // kernel timing (lsmgpu_set_kernel_timing): events before the walk, between walk and copy,
+  // after the copy of the last walk-scan-copy decode
+  hipEvent_t kev[3] = {nullptr, nullptr, nullptr};
+  bool ktime = false, kvalid = false, kfused = false;  // kfused: the last decode had no copy
 };
 
 #define HIPC(x)                                   \
@@ -128,6 +132,8 @@ void lsmgpu_close(lsmgpu_ctx* c) {
                     &c->s_bf, &c->s_bs, &c->s_a, &c->s_b, &c->s_c, &c->s_d};
   for (DevBuf* b : bufs) b->release();
   if (c->h_result) (void)hipHostFree(c->h_result);
+  for (hipEvent_t& e : c->kev)
+    if (e) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }
@@ -143,6 +149,28 @@ void* lsmgpu_get_stream(lsmgpu_ctx* c) { return c ? reinterpret_cast<void*>(c->s
 int lsmgpu_synchronize(lsmgpu_ctx* c) {
   if (!c) return LSMGPU_ERR_ARG;
   HIPC(hipStreamSynchronize(c->stream));
+  return LSMGPU_OK;
+}
+
+int lsmgpu_set_kernel_timing(lsmgpu_ctx* c, int on) {
+  if (!c) return LSMGPU_ERR_ARG;
+  HIPC(hipSetDevice(c->device));
+  if (on)
+    for (hipEvent_t& e : c->kev)
+      if (!e) HIPC(hipEventCreate(&e));
+  c->ktime = on != 0;
+  c->kvalid = false;
+  return LSMGPU_OK;
+}
+
+int lsmgpu_kernel_times(lsmgpu_ctx* c, float* walk_ms, float* copy_ms) {
+  if (!c || !walk_ms || !copy_ms) return LSMGPU_ERR_ARG;
+  if (!c->kvalid) return LSMGPU_ERR_ARG;  // no timed walk-scan-copy decode yet
+  HIPC(hipSetDevice(c->device));
+  HIPC(hipEventSynchronize(c->kev[2]));
+  HIPC(hipEventElapsedTime(walk_ms, c->kev[0], c->kev[1]));
+  HIPC(hipEventElapsedTime(copy_ms, c->kev[1], c->kev[2]));
+  if (c->kfused) *copy_ms = 0.0f;  // view-only decode finished in the walk: no copy launch
   return LSMGPU_OK;
 }
 
@@ -315,7 +343,11 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
       p.wwalk = kWalkGroup;
       p.wlanes = l == 2 || l == 4 || l == 16 ? (uint32_t)l : 8u;  // "group2" ... "group16"
     }
-    HIPC(launch_decode_wsc(p, c->stream));
+    if (c->ktime) HIPC(hipEventRecord(c->kev[0], c->stream));
+    HIPC(launch_decode_wsc(p, c->stream, c->ktime ? c->kev[1] : nullptr));
+    if (c->ktime) HIPC(hipEventRecord(c->kev[2], c->stream));
+    c->kvalid = c->ktime;
+    c->kfused = p.wfuse != 0;
     return LSMGPU_OK;
   }
   uint64_t waves = 0;

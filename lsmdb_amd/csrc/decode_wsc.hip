@@ -1167,7 +1167,7 @@ hipError_t launch_decode_tile(const DecodeParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s) {
+hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mid) {
   const uint32_t nblk = p.nblk;
   if (p.wwalk == kWalkScan)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkScan, 256>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
@@ -1185,6 +1185,7 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s) {
   else
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 256>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
   hipError_t e = hipGetLastError();
+  if (e == hipSuccess && mid) e = hipEventRecord(mid, s);
   if (e != hipSuccess || p.wfuse) return e;  // view-only: the walk wrote everything
   const uint32_t per_wg = 4 / p.wsplit;  // blocks per 4-wave workgroup
   hipLaunchKernelGGL(wsc_copy_kernel, dim3((nblk + per_wg - 1) / per_wg), dim3(256), 0, s, p);

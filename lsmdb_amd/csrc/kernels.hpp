@@ -156,7 +156,8 @@ hipError_t launch_decode(const DecodeParams& p, uint32_t max_blk_len, int num_cu
 hipError_t launch_encode(const EncodeParams& p, int num_cus, hipStream_t s);
 // walk-scan-copy decode (blocks < 64 KiB): scratch (wmeta, wstat, wbase, wstatus) sized by
 // the caller; p.gcnt[0] = 0 between launches (the walk's tile ticket), p.lb tile records
-hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s);
+// mid (optional): an event recorded between the walk and the copy launch (kernel timing)
+hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mid = nullptr);
 // fused tile decode (blocks <= 4 KiB): one launch, ticket-ordered tiles (p.gcnt[0] = 0)
 hipError_t launch_decode_tile(const DecodeParams& p, hipStream_t s);
 // fused persistent decode (blocks <= 4 KiB, decode_fsc.hip): one launch of <= num_cus

@@ -596,17 +596,19 @@ def _block_entries(block):
     return out
 
 
+@pytest.mark.parametrize("walk", ["scan", "lane", "group", "stream"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
-def test_scan_walk_adversarial(codec, oracle, monkeypatch, mode):
-    """The scan walk's header test is a filter; these blocks defeat it.  Keys and values over
-    the bytes {0, 1, 2, 3} (zero pairs everywhere, back-pointers that sometimes match), zero
-    values, fake chained headers planted inside values (a candidate whose successor's prev
-    points back at it: accepted, so verification must send the block to the serial walk), fake
-    terminators, and blocks cut short (no terminator, a torn terminator, torn entries).  Every
-    block must decode exactly as the oracle's iterator does."""
+def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
+    """Blocks built to defeat the scan walk's header filter, decoded by every walk.  Keys and
+    values use only the bytes {0, 1, 2, 3}, so zero pairs are everywhere and back-pointers
+    sometimes match.  Values are zero-filled, or carry planted fake chained headers: a
+    candidate whose successor's prev points back at it is accepted, so verification must send
+    the block to the serial walk.  Others carry fake terminators, or blocks are cut short (no
+    terminator, a torn terminator, torn entries).  Every block must decode exactly as the
+    oracle's iterator does."""
     from lsmdb_amd.codec import MODE_MATERIALIZE, MODE_VIEW
     monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
-    monkeypatch.setenv("LSMGPU_WSC_WALK", "scan")
+    monkeypatch.setenv("LSMGPU_WSC_WALK", walk)
     monkeypatch.setenv("LSMGPU_WSC_VIEWFUSE", "1")
     rng = np.random.default_rng(77)
     parts = []
@@ -650,8 +652,33 @@ def test_scan_walk_adversarial(codec, oracle, monkeypatch, mode):
         g = codec.decode_host(kd, oo, ll, mode=m)
         o = oracle.decode(kd, oo, ll)
         if mode == "materialize":
-            _assert_same(g, o, f"adversarial {sl}")
+            _assert_same(g, o, f"adversarial {walk} {sl}")
         else:
             assert g.n_entries == o.n_entries and np.array_equal(g.view, o.view)
             assert np.array_equal(g.blk_first, o.blk_first)
             assert np.array_equal(g.blk_status, o.blk_status)
+
+
+def test_kernel_times(codec, oracle, monkeypatch):
+    """lsmgpu_set_kernel_timing / lsmgpu_kernel_times: no times before a timed walk-scan-copy
+    decode; afterwards a positive walk and copy time (copy 0 for a view-only decode that ends
+    in the walk), and the timed decode's output is unchanged."""
+    from lsmdb_amd.codec import MODE_VIEW
+    monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
+    monkeypatch.setenv("LSMGPU_WSC_VIEWFUSE", "1")
+    c2 = _cols(2, 40000, seed=41)
+    data, off, ln = _sst_blocks(oracle, [oracle.build_cols(c2.keys, c2.key_end, c2.vs, c2.vs_end,
+                                                           0, 4096)[0]])
+    codec.set_kernel_timing(False)
+    with pytest.raises(Exception):
+        codec.kernel_times()
+    codec.set_kernel_timing(True)
+    try:
+        _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln), "timed")
+        walk, copy = codec.kernel_times()
+        assert walk > 0 and copy > 0
+        codec.decode_host(data, off, ln, mode=MODE_VIEW)
+        walk, copy = codec.kernel_times()
+        assert walk > 0 and copy == 0
+    finally:
+        codec.set_kernel_timing(False)
