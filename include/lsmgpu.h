@@ -62,7 +62,8 @@ int lsmgpu_synchronize(lsmgpu_ctx* ctx);
 /* Diagnostics (no reference counterpart): with timing on, walk-scan-copy decodes record HIP
  * events on the ctx's stream before the walk, between the walk and the copy, and after the
  * copy; lsmgpu_kernel_times waits for the last decode's events and returns the walk and copy
- * durations (copy 0 for view-only decodes that finish in the walk). */
+ * durations (copy 0 for view-only decodes that finish in the walk), or LSMGPU_ERR_ARG when the
+ * last decode was not timed or took another decode path. */
 int lsmgpu_set_kernel_timing(lsmgpu_ctx* ctx, int on);
 int lsmgpu_kernel_times(lsmgpu_ctx* ctx, float* walk_ms, float* copy_ms);
 const char* lsmgpu_strerror(int code);

@@ -218,6 +218,7 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
                                uint64_t nblk, uint32_t max_blk_len, int mode,
                                const lsmgpu_decoded* out, uint64_t* d_result) {
   if (!c || !out || !d_result) return LSMGPU_ERR_ARG;
+  c->kvalid = false;  // kernel times describe this decode or none (other paths record none)
   if (mode & ~(LSMGPU_MODE_MATERIALIZE | LSMGPU_MODE_VIEW)) return LSMGPU_ERR_ARG;
   if (data_len > 0xffffffffull || nblk > 0xfffffffeull) return LSMGPU_ERR_TOO_LARGE;
   HIPC(hipSetDevice(c->device));

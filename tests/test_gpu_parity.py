@@ -680,5 +680,9 @@ def test_kernel_times(codec, oracle, monkeypatch):
         codec.decode_host(data, off, ln, mode=MODE_VIEW)
         walk, copy = codec.kernel_times()
         assert walk > 0 and copy == 0
+        monkeypatch.setenv("LSMGPU_DECODE_PATH", "lds")  # another path: no (stale) times
+        codec.decode_host(data, off, ln)
+        with pytest.raises(Exception):
+            codec.kernel_times()
     finally:
         codec.set_kernel_timing(False)
