@@ -37,6 +37,8 @@ extern "C" {
 #define LSMGPU_ERR_TOO_LARGE 7  /* more than 4 GiB - 1 bytes in one call                        */
 #define LSMGPU_ERR_INTERNAL 8   /* device look-back did not converge (never expected)          */
 #define LSMGPU_ERR_NO_DEVICE 9  /* no HIP device / bad device index                            */
+#define LSMGPU_ERR_CORRUPT 10   /* compaction input: a block with a non-OK LSMGPU_BLK_* status, or
+                                   a table whose keys are not in CompareKeys order              */
 
 /* ---- per-block decode status (lsmgpu_decoded.blk_status) ---- */
 #define LSMGPU_BLK_OK 0             /* terminator, or pos >= len (iterator.go:115-118,124-127) */
@@ -102,7 +104,11 @@ typedef struct {
  * Iterator.seekToFirst/next (iterator.go:201-217,301-326) over a batch of blocks, e.g. every
  * block of the tables compactBuildTables (levels.go:239-338) merges.  blk_off/blk_len are host
  * arrays (from lsmgpu_parse_index, offsets relative to `data`).  If data_on_device is 0, `data`
- * and every output pointer are host memory and the library stages through HBM. */
+ * and every output pointer are host memory and the library stages through HBM.
+ * Size query: with every output pointer of `out` NULL the blocks are walked and n_entries,
+ * key_bytes, val_bytes, first_bad_block and n_bad_blocks report exactly what the real call
+ * needs (ent_cap >= n_entries, key_cap >= key_bytes, val_cap >= val_bytes); returns LSMGPU_OK.
+ * A real call whose buffers are too small returns LSMGPU_ERR_CAPACITY with the same needs. */
 int lsmgpu_decode_blocks(lsmgpu_ctx* ctx, const uint8_t* data, uint64_t data_len,
                          int data_on_device, const uint32_t* blk_off, const uint32_t* blk_len,
                          uint64_t nblk, int mode, lsmgpu_decoded* out);
@@ -123,7 +129,10 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* ctx, const uint8_t* d_data, uint64_t 
  * reference) or, if block_bytes > 0, before an entry that would grow a non-empty block past
  * block_bytes (opt-in knob, not in the reference).  Writes [data blocks][restarts BE32 x N]
  * [N BE32] to out; the caller appends bbloom JSON + BE32(len) exactly as builder.go:190-195.
- * restarts (host, optional) receives the block end offsets. */
+ * restarts (host, optional) receives the block end offsets.
+ * Size query: out == NULL fills *out_len / *data_len / *nrestarts from key_end / vs_end alone
+ * (keys and vs may be NULL, and ctx may be NULL for host arrays) and returns LSMGPU_OK, or the
+ * KEY_LEN / VALUE_LEN / TOO_LARGE error the real call would return. */
 int lsmgpu_encode_blocks(lsmgpu_ctx* ctx, const uint8_t* keys, const uint32_t* key_end,
                          const uint8_t* vs, const uint32_t* vs_end, uint64_t n, int on_device,
                          uint32_t entries_per_block, uint32_t block_bytes, uint8_t* out,
@@ -304,6 +313,31 @@ int lsmgpu_bloom_tables_async(lsmgpu_ctx* ctx, const uint8_t* d_keys, const uint
                               const uint32_t* tbl_first, const uint64_t* tbl_out, uint32_t ntables,
                               uint8_t* d_out, uint64_t* d_scratch, uint64_t scratch_words,
                               uint32_t* d_flags);
+
+/* ---- Whole compaction data path for tables in host memory -------------
+ * Replaces the data path of levelsController.compactBuildTables (levels.go:239-298) in one call:
+ * the input .sst images (host memory, e.g. the mmap'd files of cd.top and cd.bot) are decoded
+ * in one device batch, merged as y.NewMergeIterator(iters) (y/iterator.go:74-202) where iterator
+ * r = tables [run_first[r], run_first[r+1]) chained in order (one table per L0 top iterator,
+ * appendIteratorsReversed order; the bottom level's tables as the last run, the
+ * ConcatIterator of levels.go:252), cut where `builder.ReachedCapacity(max_table_size)` starts a
+ * new Builder (levels.go:265-271, 100 entries per block) and encoded as Finish() would
+ * (table/builder.go:163-198).  flags LSMGPU_COMPACT_BLOOM appends the restated bbloom tail to
+ * every table (complete .sst files); without it each image is Finish minus the bloom (the caller
+ * appends Go bbloom's JSONMarshal + BE32 length, byte-identical to the reference).
+ * A block with a value overflow contributes the entries before it, as Go's iterator skips the
+ * rest of that block (iterator.go:103-106,318-323); any other bad block (a Go panic) returns
+ * LSMGPU_ERR_CORRUPT.  The result stays in the ctx: *out_len bytes of images back to back and
+ * *out_tables tables; lsmgpu_compact_result copies them out.  Synchronous. */
+#define LSMGPU_COMPACT_BLOOM 1u
+int lsmgpu_compact_tables(lsmgpu_ctx* ctx, const uint8_t* const* ssts, const uint64_t* sst_len,
+                          uint32_t ntables, const uint32_t* run_first, uint32_t nruns,
+                          int64_t max_table_size, uint32_t flags, uint64_t* out_len,
+                          uint32_t* out_tables);
+/* Copies the last lsmgpu_compact_tables result: out (out_cap >= *out_len) receives the images,
+ * tbl_off (tbl_cap >= tables + 1) the offset of each table's image in out plus the end. */
+int lsmgpu_compact_result(lsmgpu_ctx* ctx, uint8_t* out, uint64_t out_cap, uint64_t* tbl_off,
+                          uint64_t tbl_cap);
 
 #ifdef __cplusplus
 }

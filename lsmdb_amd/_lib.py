@@ -26,6 +26,7 @@ ERR_VALUE_LEN = 6
 ERR_TOO_LARGE = 7
 ERR_INTERNAL = 8
 ERR_NO_DEVICE = 9
+ERR_CORRUPT = 10
 
 BLK_OK = 0
 BLK_VALUE_OVERFLOW = 1
@@ -65,7 +66,11 @@ EXPORTED_SYMBOLS = (
     "lsmgpu_encode_blocks_async",
     "lsmgpu_plan_blocks",
     "lsmgpu_encode_values",
+    "lsmgpu_compact_tables",
+    "lsmgpu_compact_result",
 )
+
+COMPACT_BLOOM = 1
 
 
 class LsmgpuDecoded(ctypes.Structure):
@@ -223,6 +228,12 @@ def _load() -> ctypes.CDLL:
     lib.lsmgpu_bloom_tables_async.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                               c_uint32, c_void_p, c_void_p, c_uint64, c_void_p]
     lib.lsmgpu_bloom_tables_async.restype = c_int
+    lib.lsmgpu_compact_tables.argtypes = [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p,
+                                          c_uint32, ctypes.c_int64, c_uint32, POINTER(c_uint64),
+                                          POINTER(c_uint32)]
+    lib.lsmgpu_compact_tables.restype = c_int
+    lib.lsmgpu_compact_result.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p, c_uint64]
+    lib.lsmgpu_compact_result.restype = c_int
     return lib
 
 

@@ -468,6 +468,27 @@ class Codec:
             self.bloom_tables_device(o, keys, key_end, o["out"], o["bloom_flags"])
         return o
 
+    # -- the whole compaction data path for host tables (levels.go:239-298)
+    def compact_host(self, ssts, run_first, max_table_size: int, bloom: bool = False) -> list:
+        """compactBuildTables' data path in one call (lsmgpu_compact_tables): input .sst images
+        (bytes), iterator r = tables [run_first[r], run_first[r+1]) in MergeIterator order;
+        returns the output tables' images (complete .sst files with bloom=True, else Finish
+        minus the bloom tail)."""
+        raws = [np.frombuffer(bytes(x) + b"\0", np.uint8) for x in ssts]
+        ptrs = (ctypes.c_void_p * max(len(raws), 1))(*[_ptr(r) for r in raws])
+        lens = np.array([r.size - 1 for r in raws] or [0], dtype=np.uint64)
+        rf = np.ascontiguousarray(run_first, dtype=np.uint32)
+        out_len, nt = c_uint64(0), ctypes.c_uint32(0)
+        check(lib().lsmgpu_compact_tables(self._ctx, ptrs, _ptr(lens), len(raws), _ptr(rf),
+                                          rf.size - 1, max_table_size,
+                                          _lib.COMPACT_BLOOM if bloom else 0, byref(out_len),
+                                          byref(nt)), "compact_tables")
+        out = np.zeros(max(out_len.value, 1), dtype=np.uint8)
+        offs = np.zeros(nt.value + 1, dtype=np.uint64)
+        check(lib().lsmgpu_compact_result(self._ctx, _ptr(out), out.size, _ptr(offs), offs.size),
+              "compact_result")
+        return [out[int(offs[t]): int(offs[t + 1])].tobytes() for t in range(nt.value)]
+
     # -- bloom tail (table/builder.go:164-195 Finish, table/table.go:301 DoesNotHave)
     def bloom_build_device(self, keys, key_end, n: int) -> dict:
         """Finish's filter over n keys WITH ts on the device (asynchronous): device tensors

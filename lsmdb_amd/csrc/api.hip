@@ -68,6 +68,13 @@ struct lsmgpu_ctx {
   // after the copy of the last walk-scan-copy decode
   hipEvent_t kev[3] = {nullptr, nullptr, nullptr};
   bool ktime = false, kvalid = false, kfused = false;  // kfused: the last decode had no copy
+  // lsmgpu_compact_tables: inputs, decoded / merged streams, cut arrays and the output images
+  // (kept on the device until lsmgpu_compact_result copies them out)
+  DevBuf cp_data, cp_off, cp_len, cp_kd, cp_ke, cp_vd, cp_ve, cp_bf, cp_bs, cp_res, cp_rf;
+  DevBuf cp_mkd, cp_mke, cp_mvd, cp_mve, cp_tf, cp_tb, cp_to, cp_out, cp_flags, cp_scratch;
+  std::vector<uint64_t> cp_tbl_out;  // ntables + 1 image offsets of the last compaction
+  uint64_t cp_bytes = 0;
+  bool cp_valid = false;
 };
 
 #define HIPC(x)                                   \
@@ -92,6 +99,7 @@ const char* lsmgpu_strerror(int code) {
     case LSMGPU_ERR_TOO_LARGE: return "more than 4 GiB - 1 bytes in one call";
     case LSMGPU_ERR_INTERNAL: return "device look-back did not converge";
     case LSMGPU_ERR_NO_DEVICE: return "no HIP device";
+    case LSMGPU_ERR_CORRUPT: return "corrupt input table (a block the iterator cannot walk)";
     default: return "unknown error";
   }
 }
@@ -129,7 +137,11 @@ void lsmgpu_close(lsmgpu_ctx* c) {
   DevBuf* bufs[] = {&c->lb, &c->result, &c->flags, &c->scan_tmp, &c->wsc,
                     &c->open_tmp, &c->merge_tmp, &c->s_data,
                     &c->s_off, &c->s_len, &c->s_kd, &c->s_ke, &c->s_vd, &c->s_ve, &c->s_view,
-                    &c->s_bf, &c->s_bs, &c->s_a, &c->s_b, &c->s_c, &c->s_d};
+                    &c->s_bf, &c->s_bs, &c->s_a, &c->s_b, &c->s_c, &c->s_d,
+                    &c->cp_data, &c->cp_off, &c->cp_len, &c->cp_kd, &c->cp_ke, &c->cp_vd,
+                    &c->cp_ve, &c->cp_bf, &c->cp_bs, &c->cp_res, &c->cp_rf, &c->cp_mkd,
+                    &c->cp_mke, &c->cp_mvd, &c->cp_mve, &c->cp_tf, &c->cp_tb, &c->cp_to,
+                    &c->cp_out, &c->cp_flags, &c->cp_scratch};
   for (DevBuf* b : bufs) b->release();
   if (c->h_result) (void)hipHostFree(c->h_result);
   for (hipEvent_t& e : c->kev)
@@ -339,8 +351,8 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
       p.wlanes = 1;
     } else if (wk_env && wk_env[0] == 's' && max_blk_len <= 4096) {
       p.wwalk = kWalkStream;
-    } else if (wk_env && wk_env[0] == 'g') {
-      const int l = atoi(wk_env + 5);
+    } else if (wk_env && strncmp(wk_env, "group", 5) == 0) {
+      const int l = atoi(wk_env + 5);  // "group" alone: 8 lanes
       p.wwalk = kWalkGroup;
       p.wlanes = l == 2 || l == 4 || l == 16 ? (uint32_t)l : 8u;  // "group2" ... "group16"
     }
@@ -373,6 +385,14 @@ int lsmgpu_decode_blocks(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
     HIPC(hipMemcpyAsync(c->s_len.p, blk_len, nblk * 4, hipMemcpyHostToDevice, c->stream));
   }
   lsmgpu_decoded d = *out;
+  // every output pointer NULL = a size query: the blocks are walked, n_entries / key_bytes /
+  // val_bytes / first_bad_block / n_bad_blocks report what a materialize (or view) call needs
+  const bool query = !out->key_data && !out->key_end && !out->val_data && !out->val_end &&
+                     !out->view && !out->blk_first && !out->blk_status;
+  if (query) {
+    d.key_cap = d.val_cap = d.ent_cap = ~0ull;
+    mode = LSMGPU_MODE_VIEW;
+  }
   const uint8_t* d_data = data;
   if (!data_on_device) {  // stage host buffers through HBM
     HIPC(c->s_data.ensure(data_len + 16));
@@ -501,10 +521,15 @@ int lsmgpu_encode_blocks(lsmgpu_ctx* c, const uint8_t* keys, const uint32_t* key
                          uint32_t epb, uint32_t block_bytes, uint8_t* out, uint64_t out_cap,
                          uint64_t* out_len, uint64_t* data_len, uint32_t* restarts,
                          uint64_t restarts_cap, uint64_t* nrestarts) {
-  if (!c || !out || !out_len) return LSMGPU_ERR_ARG;
-  if (n && (!keys || !key_end || !vs || !vs_end)) return LSMGPU_ERR_ARG;
+  if (!out_len) return LSMGPU_ERR_ARG;
+  // out == NULL is a size query: only key_end / vs_end are read (host arrays; a NULL ctx is
+  // allowed then), *out_len / *data_len / *nrestarts are filled and nothing is encoded
+  const bool query = out == nullptr;
+  if (n && (!key_end || !vs_end)) return LSMGPU_ERR_ARG;
+  if (!query && (!c || (n && (!keys || !vs)))) return LSMGPU_ERR_ARG;
+  if (query && on_device && !c) return LSMGPU_ERR_ARG;
   if (epb == 0 && block_bytes == 0) return LSMGPU_ERR_ARG;
-  HIPC(hipSetDevice(c->device));
+  if (c) HIPC(hipSetDevice(c->device));
   // host copies of the offset columns (needed for totals and the byte-target plan)
   std::vector<uint32_t> hk, hv;
   const uint32_t* hke = key_end;
@@ -542,6 +567,7 @@ int lsmgpu_encode_blocks(lsmgpu_ctx* c, const uint8_t* keys, const uint32_t* key
   if (data_len) *data_len = dl;
   if (nrestarts) *nrestarts = nb;
   if (dl > 0xffffffffull) return LSMGPU_ERR_TOO_LARGE;
+  if (query) return LSMGPU_OK;
   if (total > out_cap) return LSMGPU_ERR_CAPACITY;
 
   const uint8_t* dk = keys;
@@ -997,5 +1023,232 @@ int lsmgpu_bloom_tables_async(lsmgpu_ctx* c, const uint8_t* d_keys, const uint32
     HIPC(hipMemsetAsync(d_scratch, 0, words * 8, c->stream));
     HIPC(launch_bloom_tables(p, groups, c->stream));
   }
+  return LSMGPU_OK;
+}
+
+
+// ---- whole-compaction data path (levels.go:239-298 compactBuildTables) for host tables
+namespace {
+int compact_fail(lsmgpu_ctx* c, int rc) {
+  c->cp_valid = false;
+  return rc;
+}
+}  // namespace
+
+extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
+                                     const uint64_t* sst_len, uint32_t ntables,
+                                     const uint32_t* run_first, uint32_t nruns,
+                                     int64_t max_table_size, uint32_t flags, uint64_t* out_len,
+                                     uint32_t* out_tables) {
+  if (!c || !out_len || !out_tables) return LSMGPU_ERR_ARG;
+  *out_len = 0;
+  *out_tables = 0;
+  c->cp_valid = false;
+  if (flags & ~(uint32_t)LSMGPU_COMPACT_BLOOM) return LSMGPU_ERR_ARG;
+  if (ntables && (!ssts || !sst_len)) return LSMGPU_ERR_ARG;
+  if (!run_first || nruns == 0 || run_first[0] != 0 || run_first[nruns] != ntables)
+    return LSMGPU_ERR_ARG;
+  for (uint32_t r = 0; r < nruns; r++)
+    if (run_first[r + 1] < run_first[r]) return LSMGPU_ERR_ARG;
+  HIPC(hipSetDevice(c->device));
+  // 1. every table's tail (Table.readIndex, table.go:177-215) -> one block list over the
+  //    concatenated data regions; run r starts at block rblk[r]
+  std::vector<uint32_t> off, len;
+  std::vector<uint64_t> base(ntables + 1, 0);
+  std::vector<uint32_t> tblk(ntables + 1, 0);
+  uint32_t max_len = 0;
+  for (uint32_t t = 0; t < ntables; t++) {
+    if (!ssts[t]) return LSMGPU_ERR_ARG;
+    uint64_t nb = 0, bo = 0, bl = 0;
+    int rc = lsmgpu_parse_index(ssts[t], sst_len[t], nullptr, nullptr, 0, &nb, &bo, &bl);
+    if (rc != LSMGPU_OK && rc != LSMGPU_ERR_CAPACITY) return rc;
+    const size_t at = off.size();
+    off.resize(at + nb);
+    len.resize(at + nb);
+    rc = lsmgpu_parse_index(ssts[t], sst_len[t], off.data() + at, len.data() + at, nb, &nb, &bo, &bl);
+    if (rc != LSMGPU_OK) return rc;
+    const uint64_t dend = nb ? (uint64_t)off[at + nb - 1] + len[at + nb - 1] : 0;
+    for (uint64_t i = at; i < at + nb; i++) {
+      if (base[t] + off[i] > 0xffffffffull) return LSMGPU_ERR_TOO_LARGE;
+      off[i] += (uint32_t)base[t];
+      max_len = std::max(max_len, len[i]);
+    }
+    base[t + 1] = base[t] + dend;
+    tblk[t + 1] = (uint32_t)off.size();
+  }
+  const uint64_t nblk = off.size(), data_len = base[ntables];
+  if (data_len > 0xffffffffull) return LSMGPU_ERR_TOO_LARGE;
+  // 2. inputs to HBM, one decode over every block of every input (materialize)
+  HIPC(c->cp_data.ensure(data_len + 64));
+  for (uint32_t t = 0; t < ntables; t++)
+    if (base[t + 1] > base[t])
+      HIPC(hipMemcpyAsync(c->cp_data.as<uint8_t>() + base[t], ssts[t], base[t + 1] - base[t],
+                          hipMemcpyHostToDevice, c->stream));
+  HIPC(c->cp_off.ensure(nblk * 4 + 4));
+  HIPC(c->cp_len.ensure(nblk * 4 + 4));
+  if (nblk) {
+    HIPC(hipMemcpyAsync(c->cp_off.p, off.data(), nblk * 4, hipMemcpyHostToDevice, c->stream));
+    HIPC(hipMemcpyAsync(c->cp_len.p, len.data(), nblk * 4, hipMemcpyHostToDevice, c->stream));
+  }
+  HIPC(c->cp_res.ensure(64));
+  uint64_t* d_res = c->cp_res.as<uint64_t>();
+  uint64_t kcap = std::max<uint64_t>(data_len, 16), vcap = kcap, ecap = data_len / 10 + 1;
+  uint64_t r[8];
+  for (int attempt = 0;; attempt++) {  // plen > 0 blocks can expand keys: resize once
+    HIPC(c->cp_kd.ensure(kcap + 16));
+    HIPC(c->cp_vd.ensure(vcap + 16));
+    HIPC(c->cp_ke.ensure(ecap * 4 + 4));
+    HIPC(c->cp_ve.ensure(ecap * 4 + 4));
+    HIPC(c->cp_bf.ensure(nblk * 4 + 4));
+    HIPC(c->cp_bs.ensure(nblk * 4 + 4));
+    lsmgpu_decoded d{};
+    d.key_data = c->cp_kd.as<uint8_t>();
+    d.key_cap = kcap;
+    d.key_end = c->cp_ke.as<uint32_t>();
+    d.val_data = c->cp_vd.as<uint8_t>();
+    d.val_cap = vcap;
+    d.val_end = c->cp_ve.as<uint32_t>();
+    d.ent_cap = ecap;
+    d.blk_first = c->cp_bf.as<uint32_t>();
+    d.blk_status = c->cp_bs.as<int32_t>();
+    int rc = lsmgpu_decode_blocks_async(c, c->cp_data.as<uint8_t>(), data_len,
+                                        c->cp_off.as<uint32_t>(), c->cp_len.as<uint32_t>(), nblk,
+                                        max_len, LSMGPU_MODE_MATERIALIZE, &d, d_res);
+    if (rc != LSMGPU_OK) return rc;
+    HIPC(hipMemcpyAsync(r, d_res, 64, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    if (r[5] & 2) return LSMGPU_ERR_INTERNAL;
+    if (!(r[5] & 1)) break;
+    if (attempt) return LSMGPU_ERR_CAPACITY;
+    kcap = std::max<uint64_t>(r[1], 16);
+    vcap = std::max<uint64_t>(r[2], 16);
+    ecap = std::max<uint64_t>(r[0], 1);
+  }
+  // A value overflow ends Go's block iterator after the entries before it, and Iterator.next
+  // moves on to the next block (iterator.go:103-106,318-323): the decoded stream already holds
+  // exactly those entries.  Every other status is a Go panic / log.Fatal: corrupt input.
+  if (r[4]) {
+    std::vector<int32_t> bs(nblk);
+    HIPC(hipMemcpyAsync(bs.data(), c->cp_bs.p, nblk * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    for (int32_t s : bs)
+      if (s != LSMGPU_BLK_OK && s != LSMGPU_BLK_VALUE_OVERFLOW) return LSMGPU_ERR_CORRUPT;
+  }
+  const uint64_t n = r[0];
+  if (n > 0xfffffffeull) return LSMGPU_ERR_TOO_LARGE;
+  // 3. runs in entries: run r = the entries of tables [run_first[r], run_first[r+1])
+  std::vector<uint32_t> rf(nruns + 1);
+  {
+    std::vector<uint32_t> bf(nblk + 1);
+    HIPC(hipMemcpyAsync(bf.data(), c->cp_bf.p, (nblk + 1) * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    for (uint32_t k = 0; k <= nruns; k++) rf[k] = bf[tblk[run_first[k]]];
+  }
+  if (n == 0) {  // every input empty: the Go loop builds no table
+    c->cp_tbl_out.assign(1, 0);
+    c->cp_bytes = 0;
+    c->cp_valid = true;
+    return LSMGPU_OK;
+  }
+  HIPC(c->cp_rf.ensure((nruns + 1) * 4));
+  HIPC(hipMemcpyAsync(c->cp_rf.p, rf.data(), (nruns + 1) * 4, hipMemcpyHostToDevice, c->stream));
+  // 4. MergeIterator (y/iterator.go:74-202): lower run index wins ties, duplicates dropped
+  HIPC(c->cp_mkd.ensure(r[1] + 16));
+  HIPC(c->cp_mvd.ensure(r[2] + 16));
+  HIPC(c->cp_mke.ensure(n * 4 + 4));
+  HIPC(c->cp_mve.ensure(n * 4 + 4));
+  lsmgpu_runs runs{c->cp_kd.as<uint8_t>(), c->cp_ke.as<uint32_t>(), c->cp_vd.as<uint8_t>(),
+                   c->cp_ve.as<uint32_t>(), c->cp_rf.as<uint32_t>(), nruns, n};
+  lsmgpu_merged mo{c->cp_mkd.as<uint8_t>(), r[1] + 16, c->cp_mke.as<uint32_t>(),
+                   c->cp_mvd.as<uint8_t>(), r[2] + 16, c->cp_mve.as<uint32_t>(), nullptr, n};
+  int rc = lsmgpu_merge_runs_async(c, &runs, &mo, d_res);
+  if (rc != LSMGPU_OK) return rc;
+  uint64_t m[8];
+  HIPC(hipMemcpyAsync(m, d_res, 64, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  if (m[3] & LSMGPU_MERGE_TIMEOUT) return LSMGPU_ERR_INTERNAL;
+  if (m[3] & LSMGPU_MERGE_KEY_LEN) return LSMGPU_ERR_KEY_LEN;
+  if (m[3] & LSMGPU_MERGE_UNSORTED) return LSMGPU_ERR_CORRUPT;
+  if (m[3]) return LSMGPU_ERR_CAPACITY;
+  const uint64_t mn = m[0], mk = m[1], mv = m[2];
+  // 5. output tables where Builder.ReachedCapacity(max_table_size) starts a new builder
+  const bool bloom = (flags & LSMGPU_COMPACT_BLOOM) != 0;
+  uint64_t tcap = std::min<uint64_t>(mn, (10 * mn + mk + mv) / (uint64_t)std::max<int64_t>(max_table_size / 2, 1) + 16);
+  uint64_t cut[8];
+  for (int attempt = 0;; attempt++) {
+    HIPC(c->cp_tf.ensure((tcap + 1) * 4));
+    HIPC(c->cp_tb.ensure((tcap + 1) * 4));
+    HIPC(c->cp_to.ensure((tcap + 1) * 8));
+    rc = lsmgpu_cut_tables_ex_async(c, c->cp_mke.as<uint32_t>(), c->cp_mve.as<uint32_t>(), mn, 100,
+                                    max_table_size, bloom ? LSMGPU_CUT_BLOOM : 0u,
+                                    c->cp_tf.as<uint32_t>(), c->cp_tb.as<uint32_t>(),
+                                    c->cp_to.as<uint64_t>(), (uint32_t)tcap, d_res);
+    if (rc != LSMGPU_OK) return rc;
+    HIPC(hipMemcpyAsync(cut, d_res, 64, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    if (!cut[3]) break;
+    if (attempt || tcap >= mn) return LSMGPU_ERR_INTERNAL;
+    tcap = mn;  // one entry per table is the most there can be
+  }
+  const uint32_t nt = (uint32_t)cut[0];
+  const uint64_t bytes = cut[2];
+  // 6. every table's image in one encode launch (+ every bloom tail)
+  HIPC(c->cp_out.ensure(bytes + 16));
+  HIPC(c->cp_flags.ensure(16));
+  HIPC(hipMemsetAsync(c->cp_flags.p, 0, 16, c->stream));
+  rc = lsmgpu_encode_tables_async(c, c->cp_mkd.as<uint8_t>(), c->cp_mke.as<uint32_t>(),
+                                  c->cp_mvd.as<uint8_t>(), c->cp_mve.as<uint32_t>(), mn, mk, mv,
+                                  100, c->cp_tf.as<uint32_t>(), c->cp_tb.as<uint32_t>(),
+                                  c->cp_to.as<uint64_t>(), (uint32_t)tcap, (mn + 99) / 100 + tcap,
+                                  c->cp_out.as<uint8_t>(), c->cp_flags.as<uint32_t>());
+  if (rc != LSMGPU_OK) return rc;
+  std::vector<uint32_t> tf(nt + 1);
+  c->cp_tbl_out.assign(nt + 1, 0);
+  HIPC(hipMemcpyAsync(tf.data(), c->cp_tf.p, (nt + 1) * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipMemcpyAsync(c->cp_tbl_out.data(), c->cp_to.p, (nt + 1) * 8, hipMemcpyDeviceToHost,
+                      c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  if (bloom) {
+    uint64_t words = 8;
+    for (uint32_t g = 0; g < nt; g += kBloomSegs) {
+      uint64_t w = 0;
+      for (uint32_t t = g; t < std::min(nt, g + kBloomSegs); t++) {
+        uint64_t bits = 0, locs = 0;
+        rc = lsmgpu_bloom_params(tf[t + 1] - tf[t], &bits, &locs, nullptr);
+        if (rc != LSMGPU_OK) return rc;
+        w += bits / 64;
+      }
+      words = std::max(words, w);
+    }
+    HIPC(c->cp_scratch.ensure(words * 8));
+    rc = lsmgpu_bloom_tables_async(c, c->cp_mkd.as<uint8_t>(), c->cp_mke.as<uint32_t>(), tf.data(),
+                                   c->cp_tbl_out.data(), nt, c->cp_out.as<uint8_t>(),
+                                   c->cp_scratch.as<uint64_t>(), words,
+                                   c->cp_flags.as<uint32_t>() + 1);
+    if (rc != LSMGPU_OK) return compact_fail(c, rc);
+  }
+  uint32_t fl[4];
+  HIPC(hipMemcpyAsync(fl, c->cp_flags.p, 16, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  if ((fl[0] & 1) || (fl[1] & 1)) return LSMGPU_ERR_KEY_LEN;
+  if (fl[0] & 2) return LSMGPU_ERR_VALUE_LEN;
+  c->cp_bytes = bytes;
+  c->cp_valid = true;
+  *out_len = bytes;
+  *out_tables = nt;
+  return LSMGPU_OK;
+}
+
+extern "C" int lsmgpu_compact_result(lsmgpu_ctx* c, uint8_t* out, uint64_t out_cap,
+                                     uint64_t* tbl_off, uint64_t tbl_cap) {
+  if (!c || !c->cp_valid) return LSMGPU_ERR_ARG;
+  const uint64_t nt = c->cp_tbl_out.size() - 1;
+  if (out_cap < c->cp_bytes || tbl_cap < nt + 1) return LSMGPU_ERR_CAPACITY;
+  if ((c->cp_bytes && !out) || !tbl_off) return LSMGPU_ERR_ARG;
+  HIPC(hipSetDevice(c->device));
+  if (c->cp_bytes)
+    HIPC(hipMemcpyAsync(out, c->cp_out.p, c->cp_bytes, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  std::memcpy(tbl_off, c->cp_tbl_out.data(), (nt + 1) * 8);
   return LSMGPU_OK;
 }

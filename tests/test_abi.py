@@ -39,7 +39,7 @@ def test_exports_via_nm():
 def test_version_and_strerror():
     lib = _lib.lib()
     assert lib.lsmgpu_abi_version() == 1
-    for code in range(0, 10):
+    for code in range(0, 11):
         assert lib.lsmgpu_strerror(code)
     assert lib.lsmgpu_strerror(_lib.ERR_CAPACITY) == b"output buffer too small"
 
@@ -120,3 +120,41 @@ def test_decode_resource_budget():
     for k, v in kernels.items():
         assert v["TotalSGPRs"] <= budget, (k, v)
         assert v["ScratchSize [bytes/lane]"] == 0, (k, v)
+
+
+@pytest.mark.parametrize("cfg,n", [(1, 10000), (2, 3000), (3, 200), (5, 2000), (1, 0)])
+def test_encode_size_query_without_device(oracle, cfg, n):
+    """INTEGRATION.md's finishBlocks step 1: lsmgpu_encode_blocks with out == NULL (and a NULL
+    ctx: host arrays) reports the exact image size, data length and restart count."""
+    import ctypes
+    from ctypes import byref, c_uint64
+    if n:
+        c = workload.config_columns(cfg, n)
+        ke, ve, epb, bb = c.key_end, c.vs_end, c.entries_per_block, c.block_bytes
+        body, dl, rs = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, epb, bb)
+    else:
+        ke = ve = np.zeros(0, np.uint32)
+        epb, bb = 100, 0
+        body, dl, rs = oracle.build([], [], 100)
+    ol, dlen, nr = c_uint64(0), c_uint64(0), c_uint64(0)
+    rc = _lib.lib().lsmgpu_encode_blocks(None, None, codec._ptr(ke), None, codec._ptr(ve), ke.size,
+                                         0, epb, bb, None, 0, byref(ol), byref(dlen), None, 0,
+                                         byref(nr))
+    assert rc == _lib.OK
+    assert ol.value == len(body) and dlen.value == dl and nr.value == len(rs)
+    _ = ctypes
+
+
+def test_encode_size_query_rejects_short_key():
+    from ctypes import byref, c_uint64
+    ke = np.array([16, 24], np.uint32)  # second key is 8 B: y.ParseKey's len > 8 assertion
+    ve = np.array([5, 10], np.uint32)
+    ol, dl, nr = c_uint64(0), c_uint64(0), c_uint64(0)
+    rc = _lib.lib().lsmgpu_encode_blocks(None, None, codec._ptr(ke), None, codec._ptr(ve), 2, 0,
+                                         100, 0, None, 0, byref(ol), byref(dl), None, 0, byref(nr))
+    assert rc == _lib.ERR_KEY_LEN
+    # a real call (out != NULL) still needs a context
+    rc = _lib.lib().lsmgpu_encode_blocks(None, None, codec._ptr(ke), None, codec._ptr(ve), 2, 0,
+                                         100, 0, codec._ptr(np.zeros(64, np.uint8)), 64, byref(ol),
+                                         byref(dl), None, 0, byref(nr))
+    assert rc == _lib.ERR_ARG

@@ -1,0 +1,214 @@
+"""The cgo shim's exact call sequences, replayed through ctypes on the GPU:
+
+* decodeTable: parse_index size query -> allocate -> parse_index; decode size query (every output
+  pointer NULL) -> newDecodedBatch with the reported needs -> decode_blocks.  Checked against the
+  oracle's decode of the same blocks (table/iterator.go:93-135).
+* finishBlocks: encode_blocks size query (out == NULL) -> allocate out_len -> encode_blocks.
+  Checked byte for byte against the oracle Builder (table/builder.go:84-198).
+* compactBuildTables: lsmgpu_compact_tables -> lsmgpu_compact_result, checked against the oracle
+  MergeIterator order and the oracle Builder driven like the Go loop (levels.go:239-298).
+"""
+import ctypes
+from ctypes import byref, c_uint64
+
+import numpy as np
+import pytest
+
+import kat_defs as K
+import open_cases as C
+from lsmdb_amd import _lib, workload
+from lsmdb_amd.codec import _ptr
+
+pytestmark = pytest.mark.gpu
+
+MAT_VIEW = _lib.MODE_MATERIALIZE | _lib.MODE_VIEW
+
+
+def shim_decode_table(ctx, sst: bytes):
+    """decodeTable step by step; returns the host SoA and the query result."""
+    L = _lib.lib()
+    base = np.frombuffer(sst + b"\0", np.uint8)
+    nblk, bo, bl = c_uint64(0), c_uint64(0), c_uint64(0)
+    rc = L.lsmgpu_parse_index(_ptr(base), len(sst), None, None, 0, byref(nblk), byref(bo), byref(bl))
+    assert rc in (_lib.OK, _lib.ERR_CAPACITY)
+    off = np.zeros(max(nblk.value, 1), np.uint32)
+    ln = np.zeros(max(nblk.value, 1), np.uint32)
+    assert L.lsmgpu_parse_index(_ptr(base), len(sst), _ptr(off), _ptr(ln), nblk.value, byref(nblk),
+                                byref(bo), byref(bl)) == _lib.OK
+    n = nblk.value
+    data_end = int(off[n - 1]) + int(ln[n - 1]) if n else 0
+    q = _lib.LsmgpuDecoded()  # every output pointer NULL: the size query
+    assert L.lsmgpu_decode_blocks(ctx, _ptr(base), data_end, 0, _ptr(off), _ptr(ln), n, MAT_VIEW,
+                                  byref(q)) == _lib.OK
+    need = (q.n_entries, q.key_bytes, q.val_bytes, q.first_bad_block, q.n_bad_blocks)
+    # newDecodedBatch(entries, keyBytes, valBytes, nblk, mode): exactly the reported needs
+    kd = np.zeros(max(q.key_bytes, 1), np.uint8)
+    vd = np.zeros(max(q.val_bytes, 1), np.uint8)
+    ke = np.zeros(max(q.n_entries, 1), np.uint32)
+    ve = np.zeros(max(q.n_entries, 1), np.uint32)
+    vw = np.zeros(max(q.n_entries, 1), np.uint64)
+    bf = np.zeros(n + 1, np.uint32)
+    bs = np.zeros(max(n, 1), np.int32)
+    d = _lib.LsmgpuDecoded()
+    d.key_data, d.key_cap, d.key_end = _ptr(kd), q.key_bytes, _ptr(ke)
+    d.val_data, d.val_cap, d.val_end = _ptr(vd), q.val_bytes, _ptr(ve)
+    d.view, d.ent_cap, d.blk_first, d.blk_status = _ptr(vw), q.n_entries, _ptr(bf), _ptr(bs)
+    assert L.lsmgpu_decode_blocks(ctx, _ptr(base), data_end, 0, _ptr(off), _ptr(ln), n, MAT_VIEW,
+                                  byref(d)) == _lib.OK
+    m = d.n_entries
+    got = dict(n=m, kd=kd[: d.key_bytes].tobytes(), vd=vd[: d.val_bytes].tobytes(), ke=ke[:m],
+               ve=ve[:m], view=vw[:m], bf=bf, bs=bs[:n], fbb=d.first_bad_block, nbad=d.n_bad_blocks)
+    return got, need, off[:n], ln[:n]
+
+
+def _check_against_oracle(oracle, sst, got, need, off, ln):
+    o = oracle.decode(sst, off, ln)
+    assert need == (o.n_entries, o.key_data.size, o.val_data.size, o.first_bad_block,
+                    o.n_bad_blocks)
+    assert got["n"] == o.n_entries
+    assert got["kd"] == o.key_data.tobytes() and got["vd"] == o.val_data.tobytes()
+    assert np.array_equal(got["ke"], o.key_end) and np.array_equal(got["ve"], o.val_end)
+    assert np.array_equal(got["view"], o.view)
+    assert np.array_equal(got["bf"], o.blk_first) and np.array_equal(got["bs"], o.blk_status)
+    assert got["fbb"] == o.first_bad_block and got["nbad"] == o.n_bad_blocks
+
+
+@pytest.mark.parametrize("cfg,n", [(1, 10000), (2, 40000), (3, 3000), (5, 20000), (1, 0)])
+def test_shim_decode_table(codec, oracle, cfg, n):
+    if n:
+        c = workload.config_columns(cfg, n)
+        body, _, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, c.entries_per_block,
+                                       c.block_bytes)
+    else:
+        body, _, _ = oracle.build([], [], 100)
+    sst = body + C.TAIL
+    got, need, off, ln = shim_decode_table(codec._ctx, sst)
+    _check_against_oracle(oracle, sst, got, need, off, ln)
+
+
+def test_shim_decode_expanding_and_bad_blocks(codec, oracle):
+    """The query reports what prefix-compressed keys expand to (more key bytes than the input)
+    and the bad-block counts; the exact-size call then succeeds."""
+    blocks = [K.PLEN_BLOCK] * 40 + [kat[1] for kat in K.DECODE_KATS]
+    data = b"".join(blocks)
+    ends = np.cumsum([len(b) for b in blocks]).astype(np.uint32)
+    sst = C.with_tail(data, ends)
+    got, need, off, ln = shim_decode_table(codec._ctx, sst)
+    _check_against_oracle(oracle, sst, got, need, off, ln)
+    assert need[3] >= 0 and need[4] > 0
+
+
+@pytest.mark.parametrize("cfg,n", [(1, 10000), (2, 20000), (3, 2000), (5, 10000), (1, 0)])
+def test_shim_finish_blocks(codec, oracle, cfg, n):
+    L = _lib.lib()
+    if n:
+        c = workload.config_columns(cfg, n)
+        kb, ke, vb, ve = c.keys, c.key_end, c.vs, c.vs_end
+        epb, bb = c.entries_per_block, c.block_bytes
+    else:
+        kb, vb = np.zeros(1, np.uint8), np.zeros(1, np.uint8)
+        ke = ve = np.zeros(0, np.uint32)
+        epb, bb = 100, 0
+    out_len, data_len, nr = c_uint64(0), c_uint64(0), c_uint64(0)
+    # step 1: the size query (out == NULL)
+    assert L.lsmgpu_encode_blocks(codec._ctx, None, _ptr(ke), None, _ptr(ve), ke.size, 0, epb, bb,
+                                  None, 0, byref(out_len), byref(data_len), None, 0,
+                                  byref(nr)) == _lib.OK
+    out = np.zeros(max(out_len.value, 1), np.uint8)
+    rs = np.zeros(max(nr.value, 1), np.uint32)
+    assert L.lsmgpu_encode_blocks(codec._ctx, _ptr(kb), _ptr(ke), _ptr(vb), _ptr(ve), ke.size, 0,
+                                  epb, bb, _ptr(out), out_len.value, byref(out_len),
+                                  byref(data_len), _ptr(rs), rs.size, byref(nr)) == _lib.OK
+    if n:
+        ref, ref_dl, ref_rs = oracle.build_cols(kb, ke, vb, ve, epb, bb)
+    else:
+        ref, ref_dl, ref_rs = oracle.build([], [], 100)
+    assert out[: out_len.value].tobytes() == ref and data_len.value == ref_dl
+    assert np.array_equal(rs[: nr.value], ref_rs)
+
+
+def _tables(oracle, nt, per, seed, space=4):
+    """nt overlapping tables of one key space (updates across tables), oracle-built."""
+    out = []
+    c = workload.config_columns(space, per * 2, seed_offset=0)
+    for s in range(nt):
+        idx = np.nonzero(np.random.default_rng(seed + s).random(per * 2) < 0.5)[0]
+        keys = [bytes(c.keys[(c.key_end[i - 1] if i else 0): c.key_end[i]]) for i in idx]
+        vss = [bytes(c.vs[(c.vs_end[i - 1] if i else 0): c.vs_end[i]]) for i in idx]
+        vss = [v[:1] + bytes([s]) + v[2:] for v in vss]  # UserMeta = table: which one won a tie
+        out.append(oracle.build(keys, vss, entries_per_block=100)[0] + C.TAIL)
+    return out
+
+
+def _oracle_compaction(oracle, ssts, run_first, cap, bloom):
+    """MergeIterator over the runs (each run's tables chained, like ConcatIterator), then the Go
+    loop `if ReachedCapacity(cap) { break }; Add` per output table (levels.go:259-283)."""
+    from test_gpu_compaction import _oracle_tables
+    kd, ke, vd, ve, rf = b"", [], b"", [], [0]
+    for r in range(len(run_first) - 1):
+        for t in range(run_first[r], run_first[r + 1]):
+            off, ln, _, _ = oracle.parse_index(ssts[t])
+            d = oracle.decode(ssts[t], off, ln)
+            ke.extend((d.key_end.astype(np.int64) + len(kd)).tolist())
+            ve.extend((d.val_end.astype(np.int64) + len(vd)).tolist())
+            kd += d.key_data.tobytes()
+            vd += d.val_data.tobytes()
+        rf.append(len(ke))
+    ke, ve = np.array(ke, np.uint32), np.array(ve, np.uint32)
+    src = oracle.merge(kd, ke, np.array(rf, np.uint32))
+    ks = [kd[(ke[i - 1] if i else 0): ke[i]] for i in src]
+    vs = [vd[(ve[i - 1] if i else 0): ve[i]] for i in src]
+    return _oracle_tables(oracle, ks, vs, cap, bloom)
+
+
+@pytest.mark.parametrize("bloom", [False, True])
+@pytest.mark.parametrize("shape", ["l0", "ln"])
+def test_shim_compact_tables(codec, oracle, shape, bloom):
+    """compactBuildTables' data path in one call: L0 (every top table its own iterator, then
+    the bottom tables as one ConcatIterator run) and Ln (one top table + the bottom run)."""
+    if shape == "l0":
+        tops = _tables(oracle, 3, 8000, 70)
+        bots = _bottom_run(oracle, 4, 6000)
+        ssts = tops + bots
+        run_first = [0, 1, 2, 3, len(ssts)]
+    else:
+        tops = _tables(oracle, 1, 20000, 90)
+        bots = _bottom_run(oracle, 3, 10000)
+        ssts = tops + bots
+        run_first = [0, 1, len(ssts)]
+    cap = 1 << 20
+    got = codec.compact_host(ssts, run_first, cap, bloom=bloom)
+    want = _oracle_compaction(oracle, ssts, run_first, cap, bloom)
+    assert len(got) == len(want) >= 2
+    for k, (g, w) in enumerate(zip(got, want)):
+        assert g == w, f"table {k}"
+
+
+def _bottom_run(oracle, nt, per):
+    """nt tables with disjoint, increasing key ranges (a level >= 1: ConcatIterator input)."""
+    c = workload.config_columns(4, nt * per, seed_offset=1)
+    out = []
+    for t in range(nt):
+        keys = [bytes(c.keys[(c.key_end[i - 1] if i else 0): c.key_end[i]])
+                for i in range(t * per, (t + 1) * per)]
+        vss = [bytes(c.vs[(c.vs_end[i - 1] if i else 0): c.vs_end[i]])
+               for i in range(t * per, (t + 1) * per)]
+        out.append(oracle.build(keys, vss, entries_per_block=100)[0] + C.TAIL)
+    return out
+
+
+def test_shim_compact_empty_and_corrupt(codec, oracle):
+    L = _lib.lib()
+    empty = oracle.build([], [], 100)[0] + C.TAIL
+    assert codec.compact_host([empty, empty], [0, 1, 2], 1 << 20) == []
+    # a block whose first header has plen != 0 is a Go log.Fatal: corrupt input
+    bad = C.with_tail(K.hdr(3, 10, 5, K.NOPREV) + K.K1 + K.V1, np.array([25], np.uint32))
+    with pytest.raises(_lib.LsmgpuError) as e:
+        codec.compact_host([bad], [0, 1], 1 << 20)
+    assert e.value.code == _lib.ERR_CORRUPT
+    # a value overflow: the entries before it survive (Go's iterator skips the block's rest)
+    vo = C.with_tail(K.DECODE_KATS[5][1], np.array([len(K.DECODE_KATS[5][1])], np.uint32))
+    got = codec.compact_host([vo], [0, 1], 1 << 20)
+    want = _oracle_compaction(oracle, [vo], [0, 1], 1 << 20, False)
+    assert got == want and len(got) == 1
+    _ = (L, ctypes)
