@@ -68,6 +68,13 @@ int lsmgpu_synchronize(lsmgpu_ctx* ctx);
  * last decode was not timed or took another decode path. */
 int lsmgpu_set_kernel_timing(lsmgpu_ctx* ctx, int on);
 int lsmgpu_kernel_times(lsmgpu_ctx* ctx, float* walk_ms, float* copy_ms);
+/* Diagnostics (no reference counterpart): the practical HBM ceilings bench.py prices the decode
+ * against -- a grid-stride 16-B-per-lane streaming copy (kind 0; 2 = non-temporal loads and
+ * stores) or read (kind 1; 3 = non-temporal) of `bytes` (a multiple of 16) from d_src (to d_dst;
+ * for a read, d_dst is a 4-B sink), wg_per_cu 256-thread workgroups per CU.  Asynchronous on
+ * the ctx stream. */
+int lsmgpu_stream_probe_async(lsmgpu_ctx* ctx, int kind, const void* d_src, void* d_dst,
+                              uint64_t bytes, uint32_t wg_per_cu);
 const char* lsmgpu_strerror(int code);
 int lsmgpu_abi_version(void);
 

@@ -68,6 +68,7 @@ EXPORTED_SYMBOLS = (
     "lsmgpu_encode_values",
     "lsmgpu_compact_tables",
     "lsmgpu_compact_result",
+    "lsmgpu_stream_probe_async",
 )
 
 COMPACT_BLOOM = 1
@@ -234,6 +235,9 @@ def _load() -> ctypes.CDLL:
     lib.lsmgpu_compact_tables.restype = c_int
     lib.lsmgpu_compact_result.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p, c_uint64]
     lib.lsmgpu_compact_result.restype = c_int
+    lib.lsmgpu_stream_probe_async.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_uint64,
+                                              c_uint32]
+    lib.lsmgpu_stream_probe_async.restype = c_int
     return lib
 
 

@@ -168,6 +168,11 @@ class Codec:
               "kernel_times")
         return float(w.value), float(c.value)
 
+    def stream_probe_async(self, kind: int, src, dst, nbytes: int, wg_per_cu: int) -> None:
+        """Diagnostics: a streaming copy (kind 0 / 2 nt) or read (1 / 3 nt) of nbytes."""
+        check(lib().lsmgpu_stream_probe_async(self._ctx, kind, _ptr(src), _ptr(dst), nbytes,
+                                              wg_per_cu), "stream_probe_async")
+
     # -- decode, host buffers (table.Table path)
     def decode_host(self, data, blk_off: np.ndarray, blk_len: np.ndarray,
                     mode: int = MODE_MATERIALIZE | MODE_VIEW) -> HostDecoded:
@@ -527,6 +532,20 @@ class Codec:
         check(lib().lsmgpu_bloom_has_async(self._ctx, _ptr(bitset), bits, locs, _ptr(keys),
                                            _ptr(key_end), n, _ptr(has)), "bloom_has_async")
         return has
+
+    def bloom_has_cached(self, dev_bitset, locs: int, keys: list) -> np.ndarray:
+        """Has(key) for host keys against a filter already on the device (int64 tensor)."""
+        import torch
+        n = len(keys)
+        if n == 0:
+            return np.zeros(0, bool)
+        ke = np.cumsum([len(k) for k in keys], dtype=np.uint64).astype(np.uint32)
+        t = lambda a: torch.from_numpy(a.copy()).to(self.device)
+        kd = t(np.frombuffer(b"".join(bytes(k) for k in keys) + b"\0" * 16, np.uint8))
+        has = self.bloom_has_device(dev_bitset, int(dev_bitset.numel()) * 64, locs, kd,
+                                    t(ke.view(np.int32)), n)
+        self.synchronize()
+        return has[:n].cpu().numpy().astype(bool)
 
     def bloom_has_host(self, bitset: np.ndarray, locs: int, keys: list) -> np.ndarray:
         """Table.DoesNotHave's complement for a batch of host keys (no ts): bool array."""

@@ -186,6 +186,15 @@ int lsmgpu_kernel_times(lsmgpu_ctx* c, float* walk_ms, float* copy_ms) {
   return LSMGPU_OK;
 }
 
+int lsmgpu_stream_probe_async(lsmgpu_ctx* c, int kind, const void* d_src, void* d_dst,
+                              uint64_t bytes, uint32_t wg_per_cu) {
+  if (!c || !d_src || !d_dst || kind < 0 || kind > 3 || wg_per_cu == 0 || wg_per_cu > 64)
+    return LSMGPU_ERR_ARG;
+  HIPC(hipSetDevice(c->device));
+  HIPC(launch_stream_probe(kind, d_src, d_dst, bytes, wg_per_cu * (uint32_t)c->num_cus, c->stream));
+  return LSMGPU_OK;
+}
+
 // ------------------------------------------------------------------ index (table.go:177-215)
 int lsmgpu_parse_index(const uint8_t* sst, uint64_t len, uint32_t* blk_off, uint32_t* blk_len,
                        uint64_t cap, uint64_t* nblk, uint64_t* bloom_off, uint64_t* bloom_len) {

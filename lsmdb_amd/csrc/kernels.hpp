@@ -228,4 +228,8 @@ int decode_path(uint32_t max_blk_len, uint32_t nblk);
 hipError_t launch_values_sizes(const ValuesParams& p, hipStream_t s);
 hipError_t launch_values_write(const ValuesParams& p, hipStream_t s);
 
+// probe.hip: practical streaming ceilings (kind 0 copy, 1 read, 2 copy nt, 3 read nt)
+hipError_t launch_stream_probe(int kind, const void* src, void* dst, uint64_t bytes,
+                               uint32_t grid, hipStream_t s);
+
 }  // namespace lsmgpu

@@ -22,6 +22,13 @@ from .codec import Codec, HostDecoded, default_codec, parse_index
 from .y import MAX_U64, ValueStruct, assert_true, compare_keys, parse_key
 
 RESULT_INTERVAL = 100  # table/builder.go:13-15 resultInterval
+# Finish's bloom tail: "bbloom" = the restated bbloom filter built on the device (default);
+# "all_ones" = every bit set, so a Go reader's DoesNotHave never skips the table.  The
+# restated bbloom bytes are parity unpinned (DESIGN.md "Bloom tail"): files a Go reader opens
+# should use "all_ones" (LSMDB_AMD_BLOOM=all_ones) until they are checked against Go.
+BLOOM_BBLOOM = "bbloom"
+BLOOM_ALL_ONES = "all_ones"
+DEFAULT_BLOOM = os.environ.get("LSMDB_AMD_BLOOM", BLOOM_BBLOOM)
 MAX_U32 = 0xFFFFFFFF
 FILE_SUFFIX = ".sst"
 
@@ -49,7 +56,10 @@ class Builder:
     exactly as the reference does at every point."""
 
     def __init__(self, entries_per_block: int = RESULT_INTERVAL, block_bytes: int = 0,
-                 codec: Optional[Codec] = None):
+                 codec: Optional[Codec] = None, bloom: Optional[str] = None):
+        self.bloom = bloom or DEFAULT_BLOOM
+        if self.bloom not in (BLOOM_BBLOOM, BLOOM_ALL_ONES):
+            raise ValueError(f"bloom must be {BLOOM_BBLOOM!r} or {BLOOM_ALL_ONES!r}")
         self.entries_per_block = entries_per_block
         self.block_bytes = block_bytes
         self._codec = codec
@@ -120,7 +130,10 @@ class Builder:
             vs, vs_end = b"", np.zeros(0, np.uint32)
         body, _data_len, _restarts = codec.encode_host(keys, key_end, vs, vs_end,
                                                        self.entries_per_block, self.block_bytes)
-        bdata = codec.bloom_tail_host(keys, key_end)  # builder.go:164-181,189-195 (device)
+        if self.bloom == BLOOM_ALL_ONES:
+            bdata = _bloom.all_ones_json(n)
+        else:
+            bdata = codec.bloom_tail_host(keys, key_end)  # builder.go:164-181,189-195 (device)
         return body + bdata + struct.pack(">I", len(bdata))
 
 
@@ -150,7 +163,8 @@ class Table:
         self.biggest: Optional[bytes] = None
         self.id = 0
         self.bloom_json = b""
-        self._bloom = None  # (bitset, setLocs) once parsed
+        self._bloom = None  # (bitset, setLocs), parsed at open (table.go:186); None: Has = true
+        self._bloom_dev = None  # the bitset on the device, uploaded at the first batch probe
         self._codec: Optional[Codec] = None
         self.dec: Optional[HostDecoded] = None
         self._owns_file = False
@@ -186,16 +200,26 @@ class Table:
         return self.id
 
     def DoesNotHave(self, key: bytes) -> bool:  # noqa: N802
-        """table.go:301: !bf.Has(key), probed on the device (key as the caller passes it:
-        level_handler.go:221-224 strips the ts first)."""
-        return bool(self.DoesNotHaveBatch([key])[0])
+        """table.go:301: !bf.Has(key) (key as the caller passes it: level_handler.go:221-224
+        strips the ts first).  One key: hashed on the host, no device round trip -- it is
+        Get's cheap skip, probed once per table per lookup."""
+        if self._bloom is None:
+            return False
+        bitset, locs = self._bloom
+        return not _bloom.has(bitset, locs, bytes(key))
 
     def DoesNotHaveBatch(self, keys) -> np.ndarray:  # noqa: N802
-        """DoesNotHave for many keys in one device probe: bool array (True = not present)."""
+        """DoesNotHave for many keys in one device probe: bool array (True = not present).
+        The filter is uploaded once per Table and probed in place."""
+        keys = list(keys)
         if self._bloom is None:
-            self._bloom = _bloom.parse(self.bloom_json)  # table.go:186 JSONUnmarshal
+            return np.zeros(len(keys), bool)
         bitset, locs = self._bloom
-        return ~(self._codec or default_codec()).bloom_has_host(bitset, locs, list(keys))
+        codec = self._codec or default_codec()
+        if self._bloom_dev is None:
+            import torch
+            self._bloom_dev = torch.from_numpy(bitset.view(np.int64).copy()).to(codec.device)
+        return ~codec.bloom_has_cached(self._bloom_dev, locs, keys)
 
     def NewIterator(self, reversed: bool) -> "Iterator":  # noqa: N802
         return Iterator(self, reversed)
@@ -288,6 +312,10 @@ def _read_index(t: Table, decoder) -> None:
     raw = t.raw
     off, ln, bo, bl = parse_index(raw)
     t.bloom_json = raw[bo: bo + bl]
+    try:  # table.go:186 bbloom.JSONUnmarshal at open time
+        t._bloom = _bloom.parse(t.bloom_json)
+    except ValueError:
+        t._bloom = None  # a tail the restated parser cannot load: Has() = true (never skip)
     data_end = int(off[-1] + ln[-1]) if off.size else 0
     t.dec = decoder(np.frombuffer(raw, np.uint8)[:data_end] if data_end
                     else np.zeros(16, np.uint8), off, ln)

@@ -88,3 +88,29 @@ def test_bloom_properties(oracle):
 def test_bloom_rejects_short_keys(oracle):
     with pytest.raises(ValueError):
         oracle.bloom_build(b"12345678", np.array([8], np.uint32))
+
+
+def test_host_probe_matches_oracle(oracle):
+    """bloom.has (DoesNotHave's one-key host probe) against the oracle's sstref_bloom_has on
+    filters the oracle built (random keys, keys of every length 1..40)."""
+    import os
+    import numpy as np
+    from lsmdb_amd import bloom
+    rng = np.random.default_rng(5)
+    keys = [bytes(rng.integers(0, 256, int(rng.integers(9, 48)), dtype=np.uint8)) for _ in range(3000)]
+    kb = b"".join(keys)
+    ke = np.cumsum([len(k) for k in keys]).astype(np.uint32)
+    bs, bits, locs, ex = oracle.bloom_build(kb, ke)
+    present = [k[:-8] for k in keys[:500]]
+    absent = [os.urandom(n) for n in range(1, 41)] * 10
+    for k in present + absent:
+        assert bloom.has(bs, locs, k) == oracle.bloom_has(bs, bits, locs, ex, k), k
+    assert all(bloom.has(bs, locs, k) for k in present)
+
+
+def test_all_ones_tail_parses():
+    from lsmdb_amd import bloom
+    for n in (0, 1, 100, 519540):
+        bs, locs = bloom.parse(bloom.all_ones_json(n))
+        assert (bs == np.uint64(0xFFFFFFFFFFFFFFFF)).all() and bs.size * 64 == bloom.bbloom_params(n)[0]
+        assert bloom.has(bs, min(locs, 64), b"anything")

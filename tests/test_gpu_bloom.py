@@ -103,3 +103,31 @@ def test_table_doesnothave_roundtrip(codec, tmp_path):
     missing = [b"user%06d" % i for i in range(1, 3000, 2)]
     assert t.DoesNotHaveBatch(missing).mean() > 0.95
     t.DecrRef()
+    # one-key host probes (DoesNotHave) agree with the device batch probe key by key
+    probe = [k[:-8] for k in keys[:200]] + missing[:200]
+    batch = t.DoesNotHaveBatch(probe)
+    assert [t.DoesNotHave(k) for k in probe] == batch.tolist()
+
+
+def test_table_all_ones_tail(codec, tmp_path):
+    """Builder(bloom="all_ones"): the conservative tail for Go readers -- never a skip."""
+    from lsmdb_amd import table as T
+    from lsmdb_amd.y import ValueStruct
+    b = T.Builder(bloom=T.BLOOM_ALL_ONES, codec=codec)
+    for i in range(500):
+        b.Add(key_with_ts(b"user%06d" % i, 1), ValueStruct(meta=0x41, value=b"v"))
+    path = tmp_path / "000008.sst"
+    path.write_bytes(b.Finish())
+    t = T.OpenTable(str(path), T.MEMORY_MAP, codec=codec)
+    missing = [b"nope%06d" % i for i in range(300)]
+    assert not t.DoesNotHaveBatch(missing).any() and not t.DoesNotHave(missing[0])
+    assert sum(1 for _ in _iter(t)) == 500
+    t.DecrRef()
+
+
+def _iter(t):
+    it = t.NewIterator(False)
+    it.Rewind()
+    while it.Valid():
+        yield it.Key()
+        it.Next()

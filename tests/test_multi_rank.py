@@ -40,8 +40,9 @@ def _rank_main(rank, world, port, q):
         d = ofi.decode(sst[:data_len], off, (restarts - off).astype(np.uint32))
         ok = d.key_data.tobytes() == cols.keys.tobytes() and d.val_data.tobytes() == cols.vs.tobytes()
         wall = 0.010 * (rank + 1)                                     # rank 1 is the slow one
-        w, parity, total = bench.reduce_over_ranks(dist, torch, torch.device("cpu"), wall,
-                                                   "ok" if ok else "MISMATCH", data_len)
+        w, parity, total, per = bench.reduce_over_ranks(dist, torch, torch.device("cpu"), wall,
+                                                        "ok" if ok else "MISMATCH", data_len)
+        assert per == [0.010, 0.020]
         first_last = (cols.keys[:16].tobytes(), cols.keys[-16:].tobytes())
         q.put((rank, w, parity, total, data_len, first_last))
     finally:
@@ -73,4 +74,61 @@ def test_two_rank_shards_gloo():
 
 def test_one_rank_is_identity():
     import bench
-    assert bench.reduce_over_ranks(None, torch, None, 1.5, "ok", 123) == (1.5, "ok", 123)
+    assert bench.reduce_over_ranks(None, torch, None, 1.5, "ok", 123) == (1.5, "ok", 123, [1.5])
+
+
+def test_bench_spawns_ranks_itself():
+    """`python bench.py --gpus 2` (the driver's form without torch.distributed.run) starts two
+    ranks from a parent that never touches the GPU; with --launcher-selftest the ranks do the
+    real rank bookkeeping (gloo group, barriers, MAX / SUM / per-rank gather) around sleep
+    steps, so n_gpus and the summed bytes are checked without a GPU."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps",
+                          "5", "--launcher-selftest"], env=env, capture_output=True, text=True,
+                         timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1                          # rank 0 prints ONE line
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 2 and j["total_bytes"] == 2 << 30 and len(j["per_rank_ms"]) == 2
+    assert j["parity"] == "ok" and j["metric"].startswith("launcher self-test")
+
+
+def test_spawn_stops_ranks_when_one_fails(tmp_path):
+    """A failing rank ends the job with its exit code instead of leaving the others waiting at
+    a barrier (bench.spawn_ranks)."""
+    import bench
+    import time
+    t0 = time.time()
+    rc = bench.spawn_ranks(2, ["--gpus", "2", "--config", "9"])  # argparse rejects config 9
+    assert rc != 0 and time.time() - t0 < 120
+
+
+def test_c4_table_entries_matches_builder(oracle):
+    """bench's C4 cut (one ReachedCapacity(cap) table per GPU) equals the oracle Builder driven
+    like compactBuildTables' loop (levels.go:265-271), at small caps and the real 64 MiB."""
+    import bench
+    from lsmdb_amd import workload
+    cols = workload.config_columns(4, 6000)
+    L = oracle.lib()
+    for cap in (1 << 14, 100_000, 300_000):
+        b = L.sstref_builder_new(100, 0)
+        i = 0
+        while i < cols.n:
+            if L.sstref_builder_reached_capacity(b, cap):
+                break
+            k0 = int(cols.key_end[i - 1]) if i else 0
+            v0 = int(cols.vs_end[i - 1]) if i else 0
+            k = cols.keys[k0: int(cols.key_end[i])].tobytes()
+            v = cols.vs[v0: int(cols.vs_end[i])].tobytes()
+            L.sstref_builder_add(b, k, len(k), v, len(v))
+            i += 1
+        L.sstref_builder_free(b)
+        assert bench.c4_table_entries(cols.key_end, cols.vs_end, cap) == i
+    big = workload.config_columns(4, 560_000)
+    n = bench.c4_table_entries(big.key_end, big.vs_end, 64 << 20)
+    # SURVEY 8 quotes 519,540 entries for fixed 129-B entries; the generator mixes in 15-B value
+    # pointers and longer ExpiresAt varints, so a 64 MiB table holds a few % more
+    assert 500_000 < n < 550_000 and n < big.n
