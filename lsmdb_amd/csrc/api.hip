@@ -282,29 +282,6 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
   p.result = d_result;
   p.tag = c->tag;
   int path = decode_path(max_blk_len, (uint32_t)nblk);
-  // the fused path DMAs whole 16-B lines: it needs a 16-B aligned buffer of >= 16 B
-  if (path == 4 && (((uintptr_t)d_data & 15) != 0 || data_len < 16)) path = 2;
-  if (path == 3) {
-    static const uint32_t ablate =
-        getenv("LSMGPU_ABLATE") ? (uint32_t)atoi(getenv("LSMGPU_ABLATE")) : 0u;
-    p.ablate = ablate;
-    HIPC(launch_decode_tile(p, c->stream));
-    return LSMGPU_OK;
-  }
-  if (path == 4) {  // fused stream-walk-scan-copy: blocks <= 4 KiB
-    const size_t meta_b = (size_t)nblk * kFscRec * 4;
-    if (meta_b > c->wsc.cap) {
-      HIPC(hipStreamSynchronize(c->stream));
-      HIPC(c->wsc.ensure(meta_b));
-    }
-    p.wmeta = c->wsc.as<uint32_t>();
-    p.wcap = kFscRec;
-    static const uint32_t ablate =
-        getenv("LSMGPU_ABLATE") ? (uint32_t)atoi(getenv("LSMGPU_ABLATE")) : 0u;
-    p.ablate = ablate;
-    HIPC(launch_decode_fsc(p, c->num_cus, c->stream));
-    return LSMGPU_OK;
-  }
   if (path == 2) {  // walk-scan-copy: blocks of 4 KiB .. 64 KiB - 1
     // entries of a block (>= 10 B each) + the sentinel, rounded to 16-entry (128-B) chunks
     const uint32_t cap = (max_blk_len / 10 + 1 + 15) / 16 * 16;
@@ -339,27 +316,22 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     const char* vf_env = getenv("LSMGPU_WSC_VIEWFUSE");
     const bool fuse = vf_env ? atoi(vf_env) != 0 : nblk >= 512ull * (uint64_t)c->num_cus;
     p.wfuse = !(mode & LSMGPU_MODE_MATERIALIZE) && fuse;
-    // LSMGPU_WSC_WALK=stream: walk blocks <= 4 KiB from LDS after coalesced loads instead of
-    // lane by lane from HBM.  Measured slower (C2 1 GiB view 0.331 vs 0.313 ms, materialize
-    // 0.79 vs 0.75 ms), so the HBM walk stays the default.
     const char* wk_env = getenv("LSMGPU_WSC_WALK");
     // Default: 8 lanes per block guessing same-shape runs (kWalkGroup) when the batch has at
     // most 64 blocks per CU -- one lane per block would leave the machine idle and the walk is
     // pure latency (C4 64 MiB, 5,163 blocks: 0.106 -> 0.071 ms) -- else one lane per block
     // (C2 1 GiB: lane 0.733 vs group 0.799 ms; C5 1 GiB, 185 blocks per CU whose shapes
     // rarely repeat: lane 1.02 vs group 1.08 ms with its give-up rule, 1.66 ms without).
-    // LSMGPU_WSC_WALK=lane / group / group2 / group4 / group16 / stream / scan forces a walk
-    // (scan: a verified data-parallel header scan, VALU-bound: C2 view 0.40 vs 0.31 ms).
+    // LSMGPU_WSC_WALK=lane / group / group2 / group4 / group16 / wave forces a walk.
     p.wwalk = nblk <= 64ull * (uint64_t)c->num_cus ? kWalkGroup : kWalkLane;
     p.wlanes = p.wwalk == kWalkGroup ? 8 : 1;
     if (wk_env && wk_env[0] == 'l') {
       p.wwalk = kWalkLane;
       p.wlanes = 1;
-    } else if (wk_env && strncmp(wk_env, "scan", 4) == 0 && max_blk_len <= 4096) {
-      p.wwalk = kWalkScan;
+    } else if (wk_env && strncmp(wk_env, "wave", 4) == 0 && max_blk_len <= 4096 &&
+               data_len >= 4096) {
+      p.wwalk = kWalkWave;
       p.wlanes = 1;
-    } else if (wk_env && wk_env[0] == 's' && max_blk_len <= 4096) {
-      p.wwalk = kWalkStream;
     } else if (wk_env && strncmp(wk_env, "group", 5) == 0) {
       const int l = atoi(wk_env + 5);  // "group" alone: 8 lanes
       p.wwalk = kWalkGroup;

@@ -46,8 +46,7 @@ struct DecodeParams {
   uint32_t wj;              // walk-scan-copy: lanes per entry forced (8, 16), 0 = per block
   uint32_t wfuse;           // walk-scan-copy, view-only mode: the walk writes the view index
                             // and per-block outputs itself (no copy launch)
-  uint32_t wwalk;           // walk-scan-copy walk: kWalkLane / kWalkStream / kWalkGroup (+ lanes)
-                            // / kWalkScan
+  uint32_t wwalk;           // walk-scan-copy walk: kWalkLane / kWalkGroup (+ lanes) / kWalkWave
   uint32_t wlanes;          // kWalkGroup: lanes per block (4, 8 or 16)
 };
 
@@ -158,12 +157,6 @@ hipError_t launch_encode(const EncodeParams& p, int num_cus, hipStream_t s);
 // the caller; p.gcnt[0] = 0 between launches (the walk's tile ticket), p.lb tile records
 // mid (optional): an event recorded between the walk and the copy launch (kernel timing)
 hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mid = nullptr);
-// fused tile decode (blocks <= 4 KiB): one launch, ticket-ordered tiles (p.gcnt[0] = 0)
-hipError_t launch_decode_tile(const DecodeParams& p, hipStream_t s);
-// fused persistent decode (blocks <= 4 KiB, decode_fsc.hip): one launch of <= num_cus
-// 512-thread workgroups (one per CU, all resident), chunk aggregates in p.lb (epoch-tagged),
-// per-block u32 entry records past the 64 kept in LDS in p.wmeta at stride p.wcap = kFscRec;
-// p.data 16-B aligned, p.data_len >= 16
 // bloom tail (bloom.hip; bbloom restated, table/builder.go:164-195, table/table.go:301)
 struct BloomParams {
   const uint8_t* keys;
@@ -215,14 +208,10 @@ hipError_t launch_bloom_json(const BloomJson& p, hipStream_t s);
 
 // walk-scan-copy walk modes (DecodeParams::wwalk)
 constexpr int kWalkLane = 0;    // one lane per block, header by header from HBM
-constexpr int kWalkStream = 1;  // blocks <= 4 KiB through LDS, walked there
 constexpr int kWalkGroup = 2;   // wlanes lanes per block, speculative same-shape runs from HBM
-constexpr int kWalkScan = 3;    // blocks <= 4 KiB: a wave per block, data-parallel header scan
-constexpr uint32_t kFscRec = 412;  // 409 entries of >= 10 B in 4096 B + the sentinel, rounded
-hipError_t launch_decode_fsc(const DecodeParams& p, int num_cus, hipStream_t s);
+constexpr int kWalkWave = 4;    // blocks <= 4 KiB: LDS-DMA per wave, a speculative 64-lane walk in LDS
 // which decode path a batch takes: 0 register-lag (<= 4 KiB), 1 LDS-lag, 2 walk-scan-copy
-// (blocks < 64 KiB, batches of >= kWscMinBlocks blocks), 3 fused tile (<= 4 KiB),
-// 4 fused stream-walk-scan-copy (<= 4 KiB)
+// (blocks < 64 KiB, batches of >= kWscMinBlocks blocks)
 constexpr uint32_t kWscMinBlocks = 1024;
 int decode_path(uint32_t max_blk_len, uint32_t nblk);
 hipError_t launch_values_sizes(const ValuesParams& p, hipStream_t s);

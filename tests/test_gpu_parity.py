@@ -323,9 +323,9 @@ def test_many_rounds(codec, oracle, monkeypatch, grid, shape):
     assert g.val_data.tobytes() == cols[2].tobytes()
 
 
-@pytest.mark.parametrize("path", ["wsc", "lds", "reg", "tile", "fsc"])
+@pytest.mark.parametrize("path", ["wsc", "lds", "reg"])
 def test_forced_decode_paths(codec, oracle, monkeypatch, path):
-    """Every decode path (LSMGPU_DECODE_PATH: walk-scan-copy, LDS-lag, register-lag, fused tile) on the
+    """Every decode path (LSMGPU_DECODE_PATH: walk-scan-copy, LDS-lag, register-lag) on the
     4 KiB block shapes: C2 4 KiB blocks, short entries, the KAT blocks (every
     error status, terminators, plen > 0), prefix-compressed random blocks."""
     monkeypatch.setenv("LSMGPU_DECODE_PATH", path)
@@ -499,11 +499,11 @@ def test_wsc_lanes_per_entry(codec, oracle, monkeypatch, lanes):
     _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln), f"J={lanes}")
 
 
-@pytest.mark.parametrize("walk", ["scan", "stream", "lane", "group", "group2", "group4", "group16"])
+@pytest.mark.parametrize("walk", ["wave", "lane", "group", "group2", "group4", "group16"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
-    """Walk-scan-copy's walks (LSMGPU_WSC_WALK): blocks <= 4 KiB scanned for their headers by a
-    wave in LDS, or streamed through LDS and walked there, one lane per block from HBM, or 8 / 4
+    """Walk-scan-copy's walks (LSMGPU_WSC_WALK): blocks <= 4 KiB LDS-DMA'd and walked in LDS by
+    a whole wave speculating on entry shapes, one lane per block from HBM, or 8 / 4
     / 16 lanes per block guessing same-shape runs from HBM.  C2 /
     C3 blocks, short and tiny entries (> 64 per block), every KAT block (error statuses,
     terminators, plen > 0) at odd alignments, prefix-compressed random blocks, a ragged last
@@ -518,7 +518,7 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
              oracle.build_cols(c3.keys, c3.key_end, c3.vs, c3.vs_end, 0, 4096)[0],
              oracle.build_cols(*_random_cols(20000, 25), 0, 4096)[0],
              oracle.build_cols(*_random_cols(60000, 26, 9, 10, 3, 4), 0, 4096)[0]]
-    if walk not in ("stream", "scan"):  # LDS walks take blocks <= 4 KiB
+    if walk != "wave":  # the LDS walk takes blocks <= 4 KiB
         c5 = _cols(5, 6000, seed=27)
         parts.append(oracle.build_cols(c5.keys, c5.key_end, c5.vs, c5.vs_end, 0,
                                        c5.block_bytes)[0])
@@ -596,10 +596,10 @@ def _block_entries(block):
     return out
 
 
-@pytest.mark.parametrize("walk", ["scan", "lane", "group", "stream"])
+@pytest.mark.parametrize("walk", ["wave", "lane", "group"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
-    """Blocks built to defeat the scan walk's header filter, decoded by every walk.  Keys and
+    """Blocks built to defeat a header-pattern filter, decoded by every walk.  Keys and
     values use only the bytes {0, 1, 2, 3}, so zero pairs are everywhere and back-pointers
     sometimes match.  Values are zero-filled, or carry planted fake chained headers: a
     candidate whose successor's prev points back at it is accepted, so verification must send
