@@ -322,15 +322,11 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     // pure latency (C4 64 MiB, 5,163 blocks: 0.106 -> 0.071 ms) -- else one lane per block
     // (C2 1 GiB: lane 0.733 vs group 0.799 ms; C5 1 GiB, 185 blocks per CU whose shapes
     // rarely repeat: lane 1.02 vs group 1.08 ms with its give-up rule, 1.66 ms without).
-    // LSMGPU_WSC_WALK=lane / group / group2 / group4 / group16 / wave forces a walk.
+    // LSMGPU_WSC_WALK=lane / group / group2 / group4 / group16 forces a walk.
     p.wwalk = nblk <= 64ull * (uint64_t)c->num_cus ? kWalkGroup : kWalkLane;
     p.wlanes = p.wwalk == kWalkGroup ? 8 : 1;
     if (wk_env && wk_env[0] == 'l') {
       p.wwalk = kWalkLane;
-      p.wlanes = 1;
-    } else if (wk_env && strncmp(wk_env, "wave", 4) == 0 && max_blk_len <= 4096 &&
-               data_len >= 4096) {
-      p.wwalk = kWalkWave;
       p.wlanes = 1;
     } else if (wk_env && strncmp(wk_env, "group", 5) == 0) {
       const int l = atoi(wk_env + 5);  // "group" alone: 8 lanes

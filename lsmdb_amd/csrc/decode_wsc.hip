@@ -63,8 +63,6 @@ __device__ __forceinline__ void flush_meta(uint2* dst, const uint2* row, uint32_
   }
 }
 
-constexpr uint32_t kSwMaxLen = 4096;  // blocks the LDS (wave) walk takes
-
 // One block's walk (blockIterator.Next/parseKV, table/iterator.go:93-135) over `src` (LDS slot
 // or global bytes), writing the metadata records {header pos | value offset << 16, key offset}
 // + the sentinel straight to `meta`.  A fast loop takes plen == 0 entries (all Builder writes,
@@ -109,138 +107,6 @@ __device__ __forceinline__ WalkResult walk_meta(const Src& src, const uint8_t* f
   return WalkResult{n, K, V, st};
 }
 
-// ---- wave walk (blocks <= 4 KiB): one wave per block, walked in LDS by all 64 lanes at once
-// A wave takes 64 consecutive blocks of the tile, one after another.  Each block arrives in one
-// of the wave's kWaveSlots LDS slots by LDS-DMA (global_load_lds_dwordx4: 1 KiB per
-// instruction, coalesced, no registers), issued kWaveSlots - 1 blocks ahead, from inline asm:
-// the compiler never waits on these loads, and the wave waits for exactly the block it needs
-// with a counted `s_waitcnt vmcnt` (it knows every vector-memory instruction it issued since:
-// kWaveDma per block, one per record store).  The walk itself is speculative across the wave
-// (spec_walk): lane k reads the header at pos + k * stride, stride = the size of the last
-// accepted entry, and the wave accepts the leading run of lanes whose guess was right (every
-// entry before them had that shape) plus the first lane with a new shape -- the whole run in
-// one LDS round trip.  The first lane that fails a fast check hands the rest of the block to
-// lane 0's serial loop, which applies every stop rule of blockIterator.Next/parseKV
-// (table/iterator.go:93-135) in the iterator's order.
-constexpr uint32_t kWaveSlots = 3;     // per wave: the block being walked + 2 in flight
-constexpr uint32_t kWaveSlot = 4128;   // 258 16-B chunks: a <= 4096-B block at any 16-B shift
-                                       // + the 8-B header over-read of the fast checks
-constexpr uint32_t kWaveDma = 5;       // LDS-DMA instructions per block (chunks 0..319; the
-                                       // fifth has lanes 0-1 only: chunks 256, 257)
-constexpr uint32_t kWaveBlocks = 64;   // blocks per wave (a 256-block tile over 4 waves)
-
-// s_waitcnt vmcnt(5 * k) (k <= 8): every vector-memory instruction older than the newest 5 k
-// has completed
-__device__ __forceinline__ void vm_wait5(uint32_t k) {
-  switch (k) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(35)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
-  }
-}
-
-// Block [off, off + len) into an LDS slot: exactly kWaveDma LDS-DMA instructions whatever the
-// block (chunks past it re-read its first chunk, an L2 hit; a block outside the slot path
-// loads the buffer's first chunk, which nobody reads).  The chunk crossing the end of the data
-// buffer is never read here (it would read past the buffer): wave_fix_tail lands it.  Returns
-// whether the block needs that fix.
-__device__ __forceinline__ bool wave_dma(const DecodeParams& p, uint32_t off, uint32_t len,
-                                         uint8_t* slot, uint32_t lane) {
-  const bool fits = len <= kSwMaxLen && (uint64_t)off + len <= p.data_len;
-  const uint64_t a0 = fits ? (off & ~15ull) : 0ull;
-  const uint32_t nch = fits ? (uint32_t)(((off - a0) + len + 15) >> 4) : 1u;
-  const uint32_t safe = (uint32_t)min<uint64_t>(nch, (p.data_len - a0) >> 4);
-#pragma unroll
-  for (uint32_t k = 0; k < kWaveDma; k++) {
-    const uint32_t c = 64 * k + lane;
-    if (k + 1 < kWaveDma || lane < 2) dma16(p.data + a0 + 16ull * (c < safe ? c : 0u), slot + 1024 * k);
-  }
-  return safe < nch;
-}
-__device__ __forceinline__ void wave_fix_tail(const DecodeParams& p, uint32_t off, uint8_t* slot,
-                                              uint32_t lane) {
-  const uint64_t a0 = off & ~15ull;
-  const uint32_t c = (uint32_t)((p.data_len - a0) >> 4);  // the chunk crossing data_len
-  if (lane == 0) {
-    const uint64_t a = a0 + 16ull * c;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    for (int i = 0; i < 16; i++)
-      if (a + i < p.data_len) set_byte(v, i, p.data[a + i]);
-    *reinterpret_cast<uint4*>(slot + 16 * c) = v;
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
-// One block (len <= 4096) in an LDS slot at byte shift sh: records {pos | V << 16, K} and the
-// sentinel to meta; `stores` counts the wave's store instructions (for the counted waits).
-// The result is uniform across the wave.
-__device__ WalkResult spec_walk(const uint8_t* slot, uint32_t sh, uint32_t len, uint2* meta,
-                                uint32_t lane, uint32_t& stores) {
-  const LdsSrc src{slot, sh};
-  uint32_t pos = 0, n = 0, K = 0, V = 0;
-  uint32_t kref = 0xffffffffu, vref = 0, stride = 0;  // no shape yet: the first round takes one
-  for (;;) {
-    const uint32_t q = pos + lane * stride;  // < 2^19: pos <= 4096, stride <= 4106
-    uint32_t plen = 1, klen = 0, vlen = 0;
-    const bool inb = q + 10 <= len;
-    if (inb) {
-      const Hdr h = src.hdr(q);
-      plen = h.plen;
-      klen = h.klen;
-      vlen = h.vlen;
-    }
-    const uint32_t endq = q + 10 + klen + vlen;
-    const bool fast = inb & (klen != 0) & (plen == 0) & (endq <= len);
-    const bool same = fast & (klen == kref) & (vlen == vref);
-    const uint64_t fb = __ballot(fast), sb = __ballot(same);
-    if (!(fb & 1ull)) break;  // entry n itself needs the general loop (or the block ended)
-    const uint32_t t = sb == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~sb);  // same-shape run
-    const uint32_t m = t + ((t < 64 && ((fb >> t) & 1ull)) ? 1u : 0u);    // + a new shape
-    if (lane < m) meta[n + lane] = make_uint2(q | ((V + lane * vref) << 16), K + lane * kref);
-    stores++;
-    const uint32_t last = m - 1;  // uniform: v_readlane, not an LDS permute
-    pos = readlane(endq, last);
-    const uint32_t shape = readlane(klen | (vlen << 16), last);
-    const uint32_t nk = shape & 0xffffu, nv = shape >> 16;
-    K += t * kref * (t ? 1u : 0u) + (m > t ? nk : 0u);
-    V += t * vref * (t ? 1u : 0u) + (m > t ? nv : 0u);
-    n += m;
-    kref = nk;
-    vref = nv;
-    stride = 10 + nk + nv;
-  }
-  // general loop: every stop rule in the iterator's order, lane 0 (the result is broadcast)
-  uint32_t st = LSMGPU_BLK_OK;
-  if (lane == 0) {
-    for (;;) {
-      if (pos >= len) break;                                   // iterator.go:115-118
-      if (len - pos < 10) { st = LSMGPU_BLK_TRUNC_HEADER; break; }
-      const Hdr h = src.hdr(pos);                              // iterator.go:121
-      if ((h.klen | h.plen) == 0) break;                       // iterator.go:124-127
-      if (n == 0 && h.plen != 0) { st = LSMGPU_BLK_FIRST_PLEN; break; }  // iterator.go:129-133
-      if (10 + h.plen > len) { st = LSMGPU_BLK_PREFIX_OOB; break; }      // base key = entry 0's
-      const uint32_t end = pos + 10 + h.klen + h.vlen;         // iterator.go:101-109
-      if (end > len) { st = LSMGPU_BLK_VALUE_OVERFLOW; break; }
-      meta[n] = make_uint2(pos | (V << 16), K);
-      stores++;
-      K += h.plen + h.klen;
-      V += h.vlen;
-      n++;
-      pos = end;
-    }
-    meta[n] = make_uint2(pos | (V << 16), K);  // sentinel
-    stores++;
-  }
-  stores = readlane(stores, 0);
-  return WalkResult{readlane(n, 0), readlane(K, 0), readlane(V, 0), readlane(st, 0)};
-}
-
 // K1: lane = block; a workgroup = a tile of 256 consecutive blocks, tiles taken in ticket order
 // (p.gcnt[0]).  After the walk the workgroup scans its blocks' {entries, key bytes, value
 // bytes}, publishes the tile aggregate and finds the tile's output base by decoupled look-back
@@ -251,17 +117,13 @@ __device__ WalkResult spec_walk(const uint8_t* slot, uint32_t sh, uint32_t len, 
 // machine idle): 256 / TB lanes per block guess same-shape runs (see the branch).
 // MODE kWalkLane: lane b walks block b straight from HBM, one dependent 8-B header load per
 // entry (every 128-B line of the input is fetched on its own, as scattered requests).
-// MODE kWalkWave (blocks <= 4 KiB): wave w takes blocks [64 w, 64 w + 64) of the tile one at
-// a time, each LDS-DMA'd into a slot and walked there by all 64 lanes (see spec_walk).
 template <int MODE, uint32_t TB>  // TB = blocks per tile (<= 256 threads: thread t owns block t)
 __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   static_assert(TB <= 256, "one thread per block of the tile");
-  constexpr bool WAVEW = MODE == kWalkWave;
   constexpr uint32_t kStageBytes = 256 * kWalkStage * sizeof(uint2);
-  // group walk: a 32-record ring per block; wave walk: kWaveSlots block slots per wave (the
-  // walk's LDS also serves the view epilogue's owner map)
-  constexpr uint32_t kLdsBytes = WAVEW ? 4 * kWaveSlots * kWaveSlot
-                                 : MODE == kWalkGroup ? TB * 16 * sizeof(uint2) : kStageBytes;
+  // group walk: a 32-record ring per block (the walk's LDS also serves the view epilogue's
+  // owner map)
+  constexpr uint32_t kLdsBytes = MODE == kWalkGroup ? TB * 16 * sizeof(uint2) : kStageBytes;
   static_assert(MODE != kWalkLane || kLdsBytes == kStageBytes,
                 "the lane walk stages 16 records per lane");
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
@@ -271,7 +133,6 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   __shared__ uint32_t s_ex[3];
   __shared__ uint32_t s_first[257];  // p.wfuse: tile-relative first entry of each block
   __shared__ uint32_t s_off[MODE == kWalkGroup ? TB : 256];  // each block's input offset
-  __shared__ uint32_t s_len[WAVEW ? 256 : 1];
   constexpr uint32_t kRes = MODE == kWalkLane ? 1 : MODE == kWalkGroup ? TB : 256;
   __shared__ uint32_t s_res[4][kRes];  // group / wave walk: n, K, V, status per block
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
@@ -330,9 +191,14 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
           gK += t * kref + (m > t ? (shape & 0xffffu) : 0u);
           gV += t * vref + (m > t ? (shape >> 16) : 0u);
           gn += m;
-          kref = shape & 0xffffu;
-          vref = shape >> 16;
-          stride = 10 + kref + vref;
+          // The guess keeps the run's shape across a single odd entry (a value pointer, a longer
+          // ExpiresAt varint: the next entry usually has the common shape again) and adopts a
+          // new shape only when entry n itself broke the run (C4 walk: 0.069 -> 0.038 ms).
+          if (t == 0) {
+            kref = shape & 0xffffu;
+            vref = shape >> 16;
+            stride = 10 + kref + vref;
+          }
           rounds++;
           if (gn >= cend) {  // chunk [cend - 16, cend) complete: one full 128-B line
             __builtin_amdgcn_wave_barrier();
@@ -381,74 +247,6 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     }
     __syncthreads();
     if (b < p.nblk) {  // from here on thread t owns block tile * TB + t, as in the other walks
-      n = s_res[0][tid];
-      K = s_res[1][tid];
-      V = s_res[2][tid];
-      st = s_res[3][tid];
-      uint64_t* t = p.wstat + 3ull * b;
-      t[0] = n;
-      t[1] = K;
-      t[2] = V;
-      p.wstatus[b] = st;
-    }
-  } else if constexpr (WAVEW) {
-    static_assert(TB == 4 * kWaveBlocks, "four waves of kWaveBlocks blocks");
-    const uint32_t nb = min(TB, p.nblk - tile * TB);
-    if (b < p.nblk) {
-      s_off[tid] = p.blk_off[b];
-      s_len[tid] = p.blk_len[b];
-    }
-    __syncthreads();
-    const uint32_t i0 = wave * kWaveBlocks, i1 = min(i0 + kWaveBlocks, nb);
-    uint8_t* const slots = lds + wave * (kWaveSlots * kWaveSlot);
-    // since[j]: vector-memory instructions this wave issued after block j's DMA
-    uint32_t since[kWaveSlots] = {0, 0, 0};
-    bool tailfix[kWaveSlots] = {false, false, false};
-    auto issue = [&](uint32_t i) {
-      for (uint32_t j = 0; j < kWaveSlots; j++) since[j] += kWaveDma;
-      since[i % kWaveSlots] = 0;
-      tailfix[i % kWaveSlots] = wave_dma(p, s_off[i], s_len[i], slots + (i % kWaveSlots) * kWaveSlot, lane);
-    };
-    for (uint32_t i = i0; i < min(i0 + kWaveSlots - 1, i1); i++) issue(i);
-    for (uint32_t i = i0; i < i1; i++) {
-      if (i + kWaveSlots - 1 < i1) issue(i + kWaveSlots - 1);
-      const uint32_t sl = i % kWaveSlots;
-      vm_wait5(since[sl] / kWaveDma);  // block i has landed (a stronger wait when since > 40)
-      uint8_t* slot = slots + sl * kWaveSlot;
-      const uint32_t off = s_off[i], len = s_len[i];
-      if (tailfix[sl]) wave_fix_tail(p, off, slot, lane);
-      uint2* meta = reinterpret_cast<uint2*>(p.wmeta) + (uint64_t)(tile * TB + i) * p.wcap;
-      uint32_t stores = 0;
-      WalkResult r{0, 0, 0, LSMGPU_BLK_RANGE};
-      if ((uint64_t)off + len > p.data_len) {
-        if (lane == 0) meta[0] = make_uint2(0, 0);
-        stores = 1;
-      } else if (len > kSwMaxLen) {  // only if the caller's max_blk_len was wrong: global walk
-        if (lane == 0) r = walk_meta(GlobalSrc{p.data + off}, nullptr, len, meta);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // its stores: counted as "all done"
-        for (uint32_t j = 0; j < kWaveSlots; j++) since[j] = 0;
-        r = WalkResult{readlane(r.n, 0), readlane(r.K, 0), readlane(r.V, 0), readlane(r.status, 0)};
-      } else if (p.ablate & 4) {  // timing only: the loads alone
-        r = WalkResult{0, 0, 0, LSMGPU_BLK_OK};
-        if (lane == 0) meta[0] = make_uint2(0, 0);
-        stores = 1;
-      } else {
-        r = spec_walk(slot, off & 15u, len, meta, lane, stores);
-      }
-      for (uint32_t j = 0; j < kWaveSlots; j++) since[j] += stores;
-      if (lane == 0) {
-        s_res[0][i] = r.n;
-        s_res[1][i] = r.K;
-        s_res[2][i] = r.V;
-        s_res[3][i] = r.status;
-      }
-      // the slot is re-filled by the DMA issued at the top of iteration i + 1: every read of
-      // this block has returned (its values were used), so the LDS-DMA cannot overtake one
-    }
-    // the records are global stores of every wave: complete before the epilogue reads them
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (b < p.nblk) {
       n = s_res[0][tid];
       K = s_res[1][tid];
       V = s_res[2][tid];
@@ -752,9 +550,7 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
 
 hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mid) {
   const uint32_t nblk = p.nblk;
-  if (p.wwalk == kWalkWave)
-    hipLaunchKernelGGL((wsc_walk_kernel<kWalkWave, 256>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
-  else if (p.wwalk == kWalkGroup && p.wlanes == 2)
+  if (p.wwalk == kWalkGroup && p.wlanes == 2)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 128>), dim3((nblk + 127) / 128), dim3(256), 0, s, p);
   else if (p.wwalk == kWalkGroup && p.wlanes == 4)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 64>), dim3((nblk + 63) / 64), dim3(256), 0, s, p);

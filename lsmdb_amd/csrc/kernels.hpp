@@ -46,7 +46,7 @@ struct DecodeParams {
   uint32_t wj;              // walk-scan-copy: lanes per entry forced (8, 16), 0 = per block
   uint32_t wfuse;           // walk-scan-copy, view-only mode: the walk writes the view index
                             // and per-block outputs itself (no copy launch)
-  uint32_t wwalk;           // walk-scan-copy walk: kWalkLane / kWalkGroup (+ lanes) / kWalkWave
+  uint32_t wwalk;           // walk-scan-copy walk: kWalkLane / kWalkGroup (+ wlanes)
   uint32_t wlanes;          // kWalkGroup: lanes per block (4, 8 or 16)
 };
 
@@ -209,7 +209,6 @@ hipError_t launch_bloom_json(const BloomJson& p, hipStream_t s);
 // walk-scan-copy walk modes (DecodeParams::wwalk)
 constexpr int kWalkLane = 0;    // one lane per block, header by header from HBM
 constexpr int kWalkGroup = 2;   // wlanes lanes per block, speculative same-shape runs from HBM
-constexpr int kWalkWave = 4;    // blocks <= 4 KiB: LDS-DMA per wave, a speculative 64-lane walk in LDS
 // which decode path a batch takes: 0 register-lag (<= 4 KiB), 1 LDS-lag, 2 walk-scan-copy
 // (blocks < 64 KiB, batches of >= kWscMinBlocks blocks)
 constexpr uint32_t kWscMinBlocks = 1024;

@@ -499,11 +499,10 @@ def test_wsc_lanes_per_entry(codec, oracle, monkeypatch, lanes):
     _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln), f"J={lanes}")
 
 
-@pytest.mark.parametrize("walk", ["wave", "lane", "group", "group2", "group4", "group16"])
+@pytest.mark.parametrize("walk", ["lane", "group", "group2", "group4", "group16"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
-    """Walk-scan-copy's walks (LSMGPU_WSC_WALK): blocks <= 4 KiB LDS-DMA'd and walked in LDS by
-    a whole wave speculating on entry shapes, one lane per block from HBM, or 8 / 4
+    """Walk-scan-copy's walks (LSMGPU_WSC_WALK): one lane per block from HBM, or 8 / 4
     / 16 lanes per block guessing same-shape runs from HBM.  C2 /
     C3 blocks, short and tiny entries (> 64 per block), every KAT block (error statuses,
     terminators, plen > 0) at odd alignments, prefix-compressed random blocks, a ragged last
@@ -518,10 +517,8 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
              oracle.build_cols(c3.keys, c3.key_end, c3.vs, c3.vs_end, 0, 4096)[0],
              oracle.build_cols(*_random_cols(20000, 25), 0, 4096)[0],
              oracle.build_cols(*_random_cols(60000, 26, 9, 10, 3, 4), 0, 4096)[0]]
-    if walk != "wave":  # the LDS walk takes blocks <= 4 KiB
-        c5 = _cols(5, 6000, seed=27)
-        parts.append(oracle.build_cols(c5.keys, c5.key_end, c5.vs, c5.vs_end, 0,
-                                       c5.block_bytes)[0])
+    c5 = _cols(5, 6000, seed=27)  # + C5 32 KiB blocks
+    parts.append(oracle.build_cols(c5.keys, c5.key_end, c5.vs, c5.vs_end, 0, c5.block_bytes)[0])
     data, off, ln = _sst_blocks(oracle, parts)
     kd = bytearray(data)
     offs, lens = list(off), list(ln)
@@ -596,7 +593,7 @@ def _block_entries(block):
     return out
 
 
-@pytest.mark.parametrize("walk", ["wave", "lane", "group"])
+@pytest.mark.parametrize("walk", ["lane", "group"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
     """Blocks built to defeat a header-pattern filter, decoded by every walk.  Keys and
