@@ -243,8 +243,8 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
   if (mode & ~(LSMGPU_MODE_MATERIALIZE | LSMGPU_MODE_VIEW)) return LSMGPU_ERR_ARG;
   if (data_len > 0xffffffffull || nblk > 0xfffffffeull) return LSMGPU_ERR_TOO_LARGE;
   HIPC(hipSetDevice(c->device));
-  HIPC(hipMemsetAsync(d_result, 0, 8 * sizeof(uint64_t), c->stream));
   if (nblk == 0) {
+    HIPC(hipMemsetAsync(d_result, 0, 8 * sizeof(uint64_t), c->stream));
     if (out->blk_first) HIPC(hipMemsetAsync(out->blk_first, 0, 4, c->stream));
     return LSMGPU_OK;
   }
@@ -333,6 +333,11 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
       p.wwalk = kWalkGroup;
       p.wlanes = l == 2 || l == 4 || l == 16 ? (uint32_t)l : 8u;  // "group2" ... "group16"
     }
+    // d_result is zeroed by the walk kernel when a copy launch follows it (the copy's atomics
+    // come after the kernel boundary): one operation fewer per decode.  A view-only decode
+    // that ends in the walk updates d_result from every workgroup, so it is zeroed first.
+    if (p.wfuse) HIPC(hipMemsetAsync(d_result, 0, 8 * sizeof(uint64_t), c->stream));
+    else p.zero_result = 1;
     if (c->ktime) HIPC(hipEventRecord(c->kev[0], c->stream));
     HIPC(launch_decode_wsc(p, c->stream, c->ktime ? c->kev[1] : nullptr));
     if (c->ktime) HIPC(hipEventRecord(c->kev[2], c->stream));
@@ -341,6 +346,7 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     return LSMGPU_OK;
   }
   uint64_t waves = 0;
+  HIPC(hipMemsetAsync(d_result, 0, 8 * sizeof(uint64_t), c->stream));
   HIPC(launch_decode(p, max_blk_len, c->num_cus, c->stream, &waves));
   (void)waves;
   return LSMGPU_OK;

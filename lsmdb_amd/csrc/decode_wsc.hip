@@ -133,7 +133,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   __shared__ uint32_t s_ex[3];
   __shared__ uint32_t s_first[257];  // p.wfuse: tile-relative first entry of each block
   __shared__ uint32_t s_off[MODE == kWalkGroup ? TB : 256];  // each block's input offset
-  constexpr uint32_t kRes = MODE == kWalkLane ? 1 : MODE == kWalkGroup ? TB : 256;
+  constexpr uint32_t kRes = MODE == kWalkGroup ? TB : 1;
   __shared__ uint32_t s_res[4][kRes];  // group / wave walk: n, K, V, status per block
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t ntiles = (p.nblk + TB - 1) / TB;
@@ -142,6 +142,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     if (t == ntiles - 1) atomicExch(p.gcnt, 0u);  // every ticket is taken
     s_tile = t;
   }
+  if (p.zero_result && blockIdx.x == 0 && tid < 8) p.result[tid] = 0;  // see api.hip
   __syncthreads();
   const uint32_t tile = s_tile;
   // thread t owns block tile * TB + t (threads past TB own none: zero entries)

@@ -48,6 +48,7 @@ struct DecodeParams {
                             // and per-block outputs itself (no copy launch)
   uint32_t wwalk;           // walk-scan-copy walk: kWalkLane / kWalkGroup (+ wlanes)
   uint32_t wlanes;          // kWalkGroup: lanes per block (4, 8 or 16)
+  uint32_t zero_result;     // walk-scan-copy with a copy launch: the walk zeroes result[0..7]
 };
 
 // Encode: one wave per output block; every byte position is closed-form
