@@ -477,8 +477,8 @@ def run_rank(args) -> None:
                 "read_frac": round(w["data_len"] / (vk / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
         del vbufs
 
-    practical = practical_peaks(codec, torch, dev, w["data_len"])
-    if view is not None:
+    practical = None if args.no_peaks else practical_peaks(codec, torch, dev, w["data_len"])
+    if view is not None and practical is not None:
         view["read_frac_of_practical"] = round(
             w["data_len"] / (view["kernel_ms"] / 1e3) / 1e9 / practical["read_gbs"], 4)
     encode = time_encode(codec, torch, w, min(args.steps, 10))
@@ -521,8 +521,9 @@ def run_rank(args) -> None:
                      "traffic_ratio": round(traffic / (rd + wr), 4) if traffic else None,
                      "algorithmic_bytes_per_launch": rd + wr, "kernel_ms_mean": round(kms_mean, 4),
                      "kernel_ms_median": round(kms_med, 4),
-                     "practical_copy_gbs": practical["copy_gbs"],
-                     "frac_of_practical": round(achieved / practical["copy_gbs"], 4),
+                     "practical_copy_gbs": practical["copy_gbs"] if practical else None,
+                     "frac_of_practical": round(achieved / practical["copy_gbs"], 4)
+                     if practical else None,
                      "practical": practical,
                      "kernels": split},
         "parity": f"round-trip {parity} (decode(encode(x)) == x, all bytes and offsets)",
@@ -551,6 +552,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-view", action="store_true")
+    ap.add_argument("--no-peaks", action="store_true", help="skip the practical-peak probes "
+                    "(profiling passes); frac_of_practical is then null")
     ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
