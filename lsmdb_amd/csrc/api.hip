@@ -727,7 +727,10 @@ int lsmgpu_merge_runs_async(lsmgpu_ctx* c, const lsmgpu_runs* in, const lsmgpu_m
   const size_t dst_b = al((size_t)n * 4 + 4), flg_b = 256;
   const size_t tb_b = al(((size_t)in->nruns + 1) * 4);
   const size_t spl_b = al(((size_t)n / 256 + in->nruns) * in->nruns * 4 + 4);
-  const size_t need = dst_b + flg_b + tb_b + spl_b;
+  const size_t rec_b = al((size_t)n * 16 + 16);
+  const size_t nch = ((size_t)n + kMergeEmitTile - 1) / kMergeEmitTile;
+  const size_t occ_b = al(nch * 128 + 16), cpre_b = al(nch * 4 + 4), drop_b = al((size_t)n + 1);
+  const size_t need = dst_b + flg_b + tb_b + spl_b + rec_b + occ_b + cpre_b + drop_b;
   if (need > c->merge_tmp.cap) {
     HIPC(hipStreamSynchronize(c->stream));
     HIPC(c->merge_tmp.ensure(need));
@@ -754,6 +757,11 @@ int lsmgpu_merge_runs_async(lsmgpu_ctx* c, const lsmgpu_runs* in, const lsmgpu_m
   p.flags = reinterpret_cast<uint32_t*>(w + dst_b);
   p.tile_base = reinterpret_cast<uint32_t*>(w + dst_b + flg_b);
   p.spl = reinterpret_cast<uint32_t*>(w + dst_b + flg_b + tb_b);
+  uint8_t* w2 = w + dst_b + flg_b + tb_b + spl_b;
+  p.rec = reinterpret_cast<uint4*>(w2);
+  p.occ = reinterpret_cast<uint32_t*>(w2 + rec_b);
+  p.cpre = reinterpret_cast<uint32_t*>(w2 + rec_b + occ_b);
+  p.drop = w2 + rec_b + occ_b + cpre_b;
   p.gcnt = c->lb.as<uint32_t>();
   p.lb = reinterpret_cast<uint64_t*>(c->lb.as<uint8_t>() + 256);
   p.tag = c->tag;

@@ -131,10 +131,15 @@ struct MergeParams {
   uint32_t nruns;
   uint32_t n;                 // entries (run_first[nruns])
   uint32_t* dst;              // scratch: merged position -> entry
+  uint4* rec;                 // scratch: merged position -> {ks, kept ? kl : 0, vs, vl}
+  uint32_t* occ;              // scratch: positions taken by runs other than F (bitmap, chunks
+                              // of kMergeEmitTile bits)
+  uint32_t* cpre;             // scratch: occupied positions before each chunk
+  uint8_t* drop;              // scratch: entry -> a duplicate (an equal key comes first)
   uint32_t* gcnt;             // emit tile ticket (0 between launches, reset by the last ticket)
   uint64_t* lb;               // emit tile records (64 B per tile, epoch-tagged)
   uint64_t tag;
-  uint32_t* flags;            // scratch: [0] input errors, [1] capacity
+  uint32_t* flags;            // scratch: [0] input errors, [1] capacity, [2] fill run F
   uint32_t* tile_base;        // scratch: nruns + 1
   uint32_t* spl;              // scratch: (n / 256 + nruns) x nruns splitter ranks
   uint8_t* okd;

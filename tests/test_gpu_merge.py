@@ -112,14 +112,22 @@ def test_merge_compaction_replay(codec, oracle):
     assert gk == ek and gv == ev
 
 
-@pytest.mark.parametrize("knob,val", [("LSMGPU_MERGE_PP", "1"), ("LSMGPU_MERGE_PP", "2"),
-                                      ("LSMGPU_MERGE_G", "8")])
-def test_merge_emit_instances(codec, oracle, monkeypatch, knob, val):
-    """Every merge_emit_kernel<PP, G> instance the A/B knobs select (tiles of 256 / 512
-    positions, 8 gather pieces in flight): duplicates across and inside runs, several tiles,
-    a ragged last tile, bit-exact against the oracle MergeIterator."""
-    monkeypatch.setenv(knob, val)
-    rng = np.random.default_rng(int(val) + len(knob))
-    users = [b"u%04d" % i for i in range(900)] + [b"u01", b"u0", b"u0100"]
-    runs = [_run(rng, 1500, users, 9), _run(rng, 1300, users, 9), _run(rng, 700, users, 9)]
-    _check(codec, oracle, runs, f"{knob}={val}")
+@pytest.mark.parametrize("shape", ["fill in the middle", "fill last", "fill first",
+                                   "equal sizes", "one run with duplicates"])
+def test_merge_fill_run(codec, oracle, shape):
+    """The largest run F is never searched: its entries fill the positions the other runs'
+    ranks leave free, in order, and take their drop marks from the other runs' searches (an
+    equal key in a lower run) and from the in-run check.  F at every index, runs of equal size
+    (F = the first of them), duplicates across and inside runs, several 1024-position chunks
+    and a ragged last chunk, bit-exact against the oracle MergeIterator."""
+    rng = np.random.default_rng(len(shape))
+    users = [b"u%04d" % i for i in range(1500)] + [b"u01", b"u0", b"u0100"]
+    big = _run(rng, 5000, users, 9)
+    small = lambda: _run(rng, 700, users, 9)
+    runs = {"fill in the middle": [small(), big, small()],
+            "fill last": [small(), small(), big],
+            "fill first": [big, small(), small()],
+            "equal sizes": [_run(rng, 1500, users, 3) for _ in range(3)],
+            "one run with duplicates": [sorted(big + big[::3], key=lambda kv: (kv[0][:-8], kv[0][-8:]))],
+            }[shape]
+    _check(codec, oracle, runs, shape)
