@@ -283,6 +283,22 @@ int lsmgpu_encode_tables_async(lsmgpu_ctx* ctx, const uint8_t* d_keys, const uin
                                const uint32_t* d_tbl_blk, const uint64_t* d_tbl_out,
                                uint32_t tables_cap, uint64_t max_blocks, uint8_t* d_out,
                                uint32_t* d_flags);
+/* Gather form for a merge output without its bytes (lsmgpu_merge_runs_async with key_data =
+ * val_data = NULL, src set): entry i of the tables is source entry d_src[i] of the merge's INPUT
+ * streams (d_keys / d_key_end, d_vs / d_vs_end), placed by the merged end offsets d_out_key_end /
+ * d_out_vs_end (the merge's key_end / val_end, which the cut also read).  The bytes move once,
+ * decoded tables -> output images, as compactBuildTables' builder.Add(it.Key(), it.Value())
+ * copies them once (levels.go:273).  Images are byte-identical to lsmgpu_encode_tables_async
+ * over the gathered streams. */
+int lsmgpu_encode_tables_gather_async(lsmgpu_ctx* ctx, const uint8_t* d_keys,
+                                      const uint32_t* d_key_end, const uint8_t* d_vs,
+                                      const uint32_t* d_vs_end, const uint32_t* d_src,
+                                      const uint32_t* d_out_key_end, const uint32_t* d_out_vs_end,
+                                      uint64_t n, uint64_t key_total, uint64_t vs_total,
+                                      uint32_t entries_per_block, const uint32_t* d_tbl_first,
+                                      const uint32_t* d_tbl_blk, const uint64_t* d_tbl_out,
+                                      uint32_t tables_cap, uint64_t max_blocks, uint8_t* d_out,
+                                      uint32_t* d_flags);
 
 /* ---- Bloom tail (table/builder.go:164-195 Finish, table/table.go:180-186 readIndex, :301
  * DoesNotHave) -------------------------------------------------------------------------------
@@ -320,6 +336,13 @@ int lsmgpu_bloom_tables_async(lsmgpu_ctx* ctx, const uint8_t* d_keys, const uint
                               const uint32_t* tbl_first, const uint64_t* tbl_out, uint32_t ntables,
                               uint8_t* d_out, uint64_t* d_scratch, uint64_t scratch_words,
                               uint32_t* d_flags);
+/* Gather form (see lsmgpu_encode_tables_gather_async): key i of the tables is key d_src[i] of
+ * d_keys / d_key_end. */
+int lsmgpu_bloom_tables_gather_async(lsmgpu_ctx* ctx, const uint8_t* d_keys,
+                                     const uint32_t* d_key_end, const uint32_t* d_src,
+                                     const uint32_t* tbl_first, const uint64_t* tbl_out,
+                                     uint32_t ntables, uint8_t* d_out, uint64_t* d_scratch,
+                                     uint64_t scratch_words, uint32_t* d_flags);
 
 /* ---- Whole compaction data path for tables in host memory -------------
  * Replaces the data path of levelsController.compactBuildTables (levels.go:239-298) in one call:

@@ -60,6 +60,8 @@ EXPORTED_SYMBOLS = (
     "lsmgpu_bloom_has_async",
     "lsmgpu_cut_tables_ex_async",
     "lsmgpu_bloom_tables_async",
+    "lsmgpu_encode_tables_gather_async",
+    "lsmgpu_bloom_tables_gather_async",
     "lsmgpu_decode_blocks",
     "lsmgpu_decode_blocks_async",
     "lsmgpu_encode_blocks",
@@ -229,6 +231,16 @@ def _load() -> ctypes.CDLL:
     lib.lsmgpu_bloom_tables_async.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                               c_uint32, c_void_p, c_void_p, c_uint64, c_void_p]
     lib.lsmgpu_bloom_tables_async.restype = c_int
+    lib.lsmgpu_encode_tables_gather_async.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p,
+                                                      c_void_p, c_void_p, c_void_p, c_void_p,
+                                                      c_uint64, c_uint64, c_uint64, c_uint32,
+                                                      c_void_p, c_void_p, c_void_p, c_uint32,
+                                                      c_uint64, c_void_p, c_void_p]
+    lib.lsmgpu_encode_tables_gather_async.restype = c_int
+    lib.lsmgpu_bloom_tables_gather_async.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p,
+                                                     c_void_p, c_void_p, c_uint32, c_void_p,
+                                                     c_void_p, c_uint64, c_void_p]
+    lib.lsmgpu_bloom_tables_gather_async.restype = c_int
     lib.lsmgpu_compact_tables.argtypes = [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p,
                                           c_uint32, ctypes.c_int64, c_uint32, POINTER(c_uint64),
                                           POINTER(c_uint32)]

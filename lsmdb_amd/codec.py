@@ -422,9 +422,11 @@ class Codec:
         o["bloom"] = bloom
         return o
 
-    def bloom_tables_device(self, cut: dict, keys, key_end, out, flags) -> None:
+    def bloom_tables_device(self, cut: dict, keys, key_end, out, flags, src=None) -> None:
         """Fill the bloom tails of a bloom=True cut's tables (after encode_tables_device);
-        reads the cut's small tbl_first / tbl_out arrays back to the host (synchronizes)."""
+        reads the cut's small tbl_first / tbl_out arrays back to the host (synchronizes).
+        src: gather mode -- key i of the tables is key src[i] of keys / key_end
+        (lsmgpu_bloom_tables_gather_async)."""
         import torch
         nt = int(cut["ntables"])
         if "bloom_host" not in cut:  # the cut's arrays on the host, once
@@ -436,6 +438,12 @@ class Codec:
             cut["bloom_host"] = (tf, to, words,
                                  torch.empty(words, dtype=torch.int64, device=key_end.device))
         tf, to, words, scratch = cut["bloom_host"]
+        if src is not None:
+            check(lib().lsmgpu_bloom_tables_gather_async(self._ctx, _ptr(keys), _ptr(key_end),
+                                                         _ptr(src), _ptr(tf), _ptr(to), nt,
+                                                         _ptr(out), _ptr(scratch), words,
+                                                         _ptr(flags)), "bloom_tables_gather_async")
+            return
         check(lib().lsmgpu_bloom_tables_async(self._ctx, _ptr(keys), _ptr(key_end), _ptr(tf),
                                               _ptr(to), nt, _ptr(out), _ptr(scratch), words,
                                               _ptr(flags)), "bloom_tables_async")
@@ -449,6 +457,19 @@ class Codec:
                                                _ptr(cut["tbl_first"]), _ptr(cut["tbl_blk"]),
                                                _ptr(cut["tbl_out"]), tc, (n + epb - 1) // epb + tc,
                                                _ptr(out), _ptr(flags)), "encode_tables_async")
+
+    def encode_tables_gather_device(self, cut: dict, keys, key_end, vs, vs_end, src,
+                                    out_key_end, out_vs_end, key_total: int, vs_total: int, out,
+                                    flags) -> None:
+        """lsmgpu_encode_tables_gather_async over a cut (asynchronous): table entry i is source
+        entry src[i] of keys / key_end, vs / vs_end, placed by the merged ends out_key_end /
+        out_vs_end (a merge_device(..., gather=False) output)."""
+        n, epb, tc = cut["n"], cut["epb"], cut["tables_cap"]
+        check(lib().lsmgpu_encode_tables_gather_async(
+            self._ctx, _ptr(keys), _ptr(key_end), _ptr(vs), _ptr(vs_end), _ptr(src),
+            _ptr(out_key_end), _ptr(out_vs_end), n, key_total, vs_total, epb,
+            _ptr(cut["tbl_first"]), _ptr(cut["tbl_blk"]), _ptr(cut["tbl_out"]), tc,
+            (n + epb - 1) // epb + tc, _ptr(out), _ptr(flags)), "encode_tables_gather_async")
 
     def compact_tables_device(self, keys, key_end, vs, vs_end, n: int, key_total: int,
                               vs_total: int, cap: int, entries_per_block: int = 100,

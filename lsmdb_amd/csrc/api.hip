@@ -71,7 +71,7 @@ struct lsmgpu_ctx {
   // lsmgpu_compact_tables: inputs, decoded / merged streams, cut arrays and the output images
   // (kept on the device until lsmgpu_compact_result copies them out)
   DevBuf cp_data, cp_off, cp_len, cp_kd, cp_ke, cp_vd, cp_ve, cp_bf, cp_bs, cp_res, cp_rf;
-  DevBuf cp_mkd, cp_mke, cp_mvd, cp_mve, cp_tf, cp_tb, cp_to, cp_out, cp_flags, cp_scratch;
+  DevBuf cp_msrc, cp_mke, cp_mve, cp_tf, cp_tb, cp_to, cp_out, cp_flags, cp_scratch;
   std::vector<uint64_t> cp_tbl_out;  // ntables + 1 image offsets of the last compaction
   uint64_t cp_bytes = 0;
   bool cp_valid = false;
@@ -139,8 +139,8 @@ void lsmgpu_close(lsmgpu_ctx* c) {
                     &c->s_off, &c->s_len, &c->s_kd, &c->s_ke, &c->s_vd, &c->s_ve, &c->s_view,
                     &c->s_bf, &c->s_bs, &c->s_a, &c->s_b, &c->s_c, &c->s_d,
                     &c->cp_data, &c->cp_off, &c->cp_len, &c->cp_kd, &c->cp_ke, &c->cp_vd,
-                    &c->cp_ve, &c->cp_bf, &c->cp_bs, &c->cp_res, &c->cp_rf, &c->cp_mkd,
-                    &c->cp_mke, &c->cp_mvd, &c->cp_mve, &c->cp_tf, &c->cp_tb, &c->cp_to,
+                    &c->cp_ve, &c->cp_bf, &c->cp_bs, &c->cp_res, &c->cp_rf, &c->cp_msrc,
+                    &c->cp_mke, &c->cp_mve, &c->cp_tf, &c->cp_tb, &c->cp_to,
                     &c->cp_out, &c->cp_flags, &c->cp_scratch};
   for (DevBuf* b : bufs) b->release();
   if (c->h_result) (void)hipHostFree(c->h_result);
@@ -818,24 +818,34 @@ int lsmgpu_cut_tables_ex_async(lsmgpu_ctx* c, const uint32_t* d_key_end, const u
   return LSMGPU_OK;
 }
 
-int lsmgpu_encode_tables_async(lsmgpu_ctx* c, const uint8_t* d_keys, const uint32_t* d_key_end,
-                               const uint8_t* d_vs, const uint32_t* d_vs_end, uint64_t n,
-                               uint64_t key_total, uint64_t vs_total,
-                               uint32_t entries_per_block, const uint32_t* d_tbl_first,
-                               const uint32_t* d_tbl_blk, const uint64_t* d_tbl_out,
-                               uint32_t tables_cap, uint64_t max_blocks, uint8_t* d_out,
-                               uint32_t* d_flags) {
+namespace {
+int encode_tables_impl(lsmgpu_ctx* c, const uint8_t* d_keys, const uint32_t* d_key_end,
+                  const uint8_t* d_vs, const uint32_t* d_vs_end, const uint32_t* d_src,
+                  const uint32_t* d_out_key_end, const uint32_t* d_out_vs_end, uint64_t n,
+                  uint64_t key_total, uint64_t vs_total, uint32_t entries_per_block,
+                  const uint32_t* d_tbl_first, const uint32_t* d_tbl_blk,
+                  const uint64_t* d_tbl_out, uint32_t tables_cap, uint64_t max_blocks,
+                  uint8_t* d_out, uint32_t* d_flags) {
   if (!c || !d_tbl_first || !d_tbl_blk || !d_tbl_out || !d_out || !d_flags) return LSMGPU_ERR_ARG;
   if (n && (!d_keys || !d_key_end || !d_vs || !d_vs_end)) return LSMGPU_ERR_ARG;
+  if (n && d_src && (!d_out_key_end || !d_out_vs_end)) return LSMGPU_ERR_ARG;
   if (entries_per_block == 0 || tables_cap == 0) return LSMGPU_ERR_ARG;
   if (max_blocks > 0xffffffffull || n > 0xffffffffull) return LSMGPU_ERR_TOO_LARGE;
   if (n == 0) return LSMGPU_OK;
   HIPC(hipSetDevice(c->device));
   EncodeParams p{};
   p.keys = d_keys;
-  p.key_end = d_key_end;
   p.vs = d_vs;
-  p.vs_end = d_vs_end;
+  if (d_src) {  // gather: placed by the merged ends, bytes read at the source entries
+    p.key_end = d_out_key_end;
+    p.vs_end = d_out_vs_end;
+    p.src = d_src;
+    p.src_key_end = d_key_end;
+    p.src_vs_end = d_vs_end;
+  } else {
+    p.key_end = d_key_end;
+    p.vs_end = d_vs_end;
+  }
   p.n = n;
   p.key_total = key_total;
   p.vs_total = vs_total;
@@ -849,6 +859,34 @@ int lsmgpu_encode_tables_async(lsmgpu_ctx* c, const uint8_t* d_keys, const uint3
   p.ntables = tables_cap;  // the kernel reads the real count from the arrays' closing entries
   HIPC(launch_encode(p, c->num_cus, c->stream));
   return LSMGPU_OK;
+}
+}  // namespace
+
+int lsmgpu_encode_tables_async(lsmgpu_ctx* c, const uint8_t* d_keys, const uint32_t* d_key_end,
+                               const uint8_t* d_vs, const uint32_t* d_vs_end, uint64_t n,
+                               uint64_t key_total, uint64_t vs_total,
+                               uint32_t entries_per_block, const uint32_t* d_tbl_first,
+                               const uint32_t* d_tbl_blk, const uint64_t* d_tbl_out,
+                               uint32_t tables_cap, uint64_t max_blocks, uint8_t* d_out,
+                               uint32_t* d_flags) {
+  return encode_tables_impl(c, d_keys, d_key_end, d_vs, d_vs_end, nullptr, nullptr, nullptr, n,
+                       key_total, vs_total, entries_per_block, d_tbl_first, d_tbl_blk, d_tbl_out,
+                       tables_cap, max_blocks, d_out, d_flags);
+}
+
+int lsmgpu_encode_tables_gather_async(lsmgpu_ctx* c, const uint8_t* d_keys,
+                                      const uint32_t* d_key_end, const uint8_t* d_vs,
+                                      const uint32_t* d_vs_end, const uint32_t* d_src,
+                                      const uint32_t* d_out_key_end, const uint32_t* d_out_vs_end,
+                                      uint64_t n, uint64_t key_total, uint64_t vs_total,
+                                      uint32_t entries_per_block, const uint32_t* d_tbl_first,
+                                      const uint32_t* d_tbl_blk, const uint64_t* d_tbl_out,
+                                      uint32_t tables_cap, uint64_t max_blocks, uint8_t* d_out,
+                                      uint32_t* d_flags) {
+  if (n && !d_src) return LSMGPU_ERR_ARG;
+  return encode_tables_impl(c, d_keys, d_key_end, d_vs, d_vs_end, d_src, d_out_key_end, d_out_vs_end,
+                       n, key_total, vs_total, entries_per_block, d_tbl_first, d_tbl_blk,
+                       d_tbl_out, tables_cap, max_blocks, d_out, d_flags);
 }
 
 }  // extern "C"
@@ -965,10 +1003,36 @@ int lsmgpu_bloom_has_async(lsmgpu_ctx* c, const uint64_t* d_bitset, uint64_t bit
   return LSMGPU_OK;
 }
 
+namespace {
+int bloom_tables_impl(lsmgpu_ctx* c, const uint8_t* d_keys, const uint32_t* d_key_end,
+                 const uint32_t* d_src, const uint32_t* tbl_first, const uint64_t* tbl_out,
+                 uint32_t ntables, uint8_t* d_out, uint64_t* d_scratch, uint64_t scratch_words,
+                 uint32_t* d_flags);
+}  // namespace
+
 int lsmgpu_bloom_tables_async(lsmgpu_ctx* c, const uint8_t* d_keys, const uint32_t* d_key_end,
                               const uint32_t* tbl_first, const uint64_t* tbl_out, uint32_t ntables,
                               uint8_t* d_out, uint64_t* d_scratch, uint64_t scratch_words,
                               uint32_t* d_flags) {
+  return bloom_tables_impl(c, d_keys, d_key_end, nullptr, tbl_first, tbl_out, ntables, d_out,
+                      d_scratch, scratch_words, d_flags);
+}
+
+int lsmgpu_bloom_tables_gather_async(lsmgpu_ctx* c, const uint8_t* d_keys,
+                                     const uint32_t* d_key_end, const uint32_t* d_src,
+                                     const uint32_t* tbl_first, const uint64_t* tbl_out,
+                                     uint32_t ntables, uint8_t* d_out, uint64_t* d_scratch,
+                                     uint64_t scratch_words, uint32_t* d_flags) {
+  if (ntables && !d_src) return LSMGPU_ERR_ARG;
+  return bloom_tables_impl(c, d_keys, d_key_end, d_src, tbl_first, tbl_out, ntables, d_out, d_scratch,
+                      scratch_words, d_flags);
+}
+
+namespace {
+int bloom_tables_impl(lsmgpu_ctx* c, const uint8_t* d_keys, const uint32_t* d_key_end,
+                 const uint32_t* d_src, const uint32_t* tbl_first, const uint64_t* tbl_out,
+                 uint32_t ntables, uint8_t* d_out, uint64_t* d_scratch, uint64_t scratch_words,
+                 uint32_t* d_flags) {
   if (!c || !tbl_first || !tbl_out || !d_out || !d_scratch || !d_flags) return LSMGPU_ERR_ARG;
   if (ntables && (!d_keys || !d_key_end)) return LSMGPU_ERR_ARG;
   HIPC(hipSetDevice(c->device));
@@ -979,6 +1043,7 @@ int lsmgpu_bloom_tables_async(lsmgpu_ctx* c, const uint8_t* d_keys, const uint32
     BloomTables p{};
     p.keys = d_keys;
     p.key_end = d_key_end;
+    p.src = d_src;
     p.scratch = d_scratch;
     p.out = d_out;
     p.flags = d_flags;
@@ -1016,6 +1081,7 @@ int lsmgpu_bloom_tables_async(lsmgpu_ctx* c, const uint8_t* d_keys, const uint32
   }
   return LSMGPU_OK;
 }
+}  // namespace
 
 
 // ---- whole-compaction data path (levels.go:239-298 compactBuildTables) for host tables
@@ -1144,14 +1210,15 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
   HIPC(c->cp_rf.ensure((nruns + 1) * 4));
   HIPC(hipMemcpyAsync(c->cp_rf.p, rf.data(), (nruns + 1) * 4, hipMemcpyHostToDevice, c->stream));
   // 4. MergeIterator (y/iterator.go:74-202): lower run index wins ties, duplicates dropped
-  HIPC(c->cp_mkd.ensure(r[1] + 16));
-  HIPC(c->cp_mvd.ensure(r[2] + 16));
+  // the merge writes the merged order (source index + end offsets), not the bytes: the
+  // encoder reads each entry's bytes from the decoded tables, the one copy builder.Add makes
+  HIPC(c->cp_msrc.ensure(n * 4 + 4));
   HIPC(c->cp_mke.ensure(n * 4 + 4));
   HIPC(c->cp_mve.ensure(n * 4 + 4));
   lsmgpu_runs runs{c->cp_kd.as<uint8_t>(), c->cp_ke.as<uint32_t>(), c->cp_vd.as<uint8_t>(),
                    c->cp_ve.as<uint32_t>(), c->cp_rf.as<uint32_t>(), nruns, n};
-  lsmgpu_merged mo{c->cp_mkd.as<uint8_t>(), r[1] + 16, c->cp_mke.as<uint32_t>(),
-                   c->cp_mvd.as<uint8_t>(), r[2] + 16, c->cp_mve.as<uint32_t>(), nullptr, n};
+  lsmgpu_merged mo{nullptr, 0, c->cp_mke.as<uint32_t>(), nullptr, 0, c->cp_mve.as<uint32_t>(),
+                   c->cp_msrc.as<uint32_t>(), n};
   int rc = lsmgpu_merge_runs_async(c, &runs, &mo, d_res);
   if (rc != LSMGPU_OK) return rc;
   uint64_t m[8];
@@ -1187,11 +1254,14 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
   HIPC(c->cp_out.ensure(bytes + 16));
   HIPC(c->cp_flags.ensure(16));
   HIPC(hipMemsetAsync(c->cp_flags.p, 0, 16, c->stream));
-  rc = lsmgpu_encode_tables_async(c, c->cp_mkd.as<uint8_t>(), c->cp_mke.as<uint32_t>(),
-                                  c->cp_mvd.as<uint8_t>(), c->cp_mve.as<uint32_t>(), mn, mk, mv,
-                                  100, c->cp_tf.as<uint32_t>(), c->cp_tb.as<uint32_t>(),
-                                  c->cp_to.as<uint64_t>(), (uint32_t)tcap, (mn + 99) / 100 + tcap,
-                                  c->cp_out.as<uint8_t>(), c->cp_flags.as<uint32_t>());
+  rc = lsmgpu_encode_tables_gather_async(c, c->cp_kd.as<uint8_t>(), c->cp_ke.as<uint32_t>(),
+                                         c->cp_vd.as<uint8_t>(), c->cp_ve.as<uint32_t>(),
+                                         c->cp_msrc.as<uint32_t>(), c->cp_mke.as<uint32_t>(),
+                                         c->cp_mve.as<uint32_t>(), mn, mk, mv, 100,
+                                         c->cp_tf.as<uint32_t>(), c->cp_tb.as<uint32_t>(),
+                                         c->cp_to.as<uint64_t>(), (uint32_t)tcap,
+                                         (mn + 99) / 100 + tcap, c->cp_out.as<uint8_t>(),
+                                         c->cp_flags.as<uint32_t>());
   if (rc != LSMGPU_OK) return rc;
   std::vector<uint32_t> tf(nt + 1);
   c->cp_tbl_out.assign(nt + 1, 0);
@@ -1212,10 +1282,11 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
       words = std::max(words, w);
     }
     HIPC(c->cp_scratch.ensure(words * 8));
-    rc = lsmgpu_bloom_tables_async(c, c->cp_mkd.as<uint8_t>(), c->cp_mke.as<uint32_t>(), tf.data(),
-                                   c->cp_tbl_out.data(), nt, c->cp_out.as<uint8_t>(),
-                                   c->cp_scratch.as<uint64_t>(), words,
-                                   c->cp_flags.as<uint32_t>() + 1);
+    rc = lsmgpu_bloom_tables_gather_async(c, c->cp_kd.as<uint8_t>(), c->cp_ke.as<uint32_t>(),
+                                          c->cp_msrc.as<uint32_t>(), tf.data(),
+                                          c->cp_tbl_out.data(), nt, c->cp_out.as<uint8_t>(),
+                                          c->cp_scratch.as<uint64_t>(), words,
+                                          c->cp_flags.as<uint32_t>() + 1);
     if (rc != LSMGPU_OK) return compact_fail(c, rc);
   }
   uint32_t fl[4];

@@ -148,7 +148,8 @@ __global__ void __launch_bounds__(256) bloom_tables_build_kernel(BloomTables p) 
   if (gi >= p.end) return;
   const uint32_t i = (uint32_t)gi;
   const BloomSeg& sg = p.seg[seg_of_key(p, i)];
-  const uint32_t s = i ? p.key_end[i - 1] : 0u, e = p.key_end[i];
+  const uint32_t ki = p.src ? p.src[i] : i;  // gather mode: the merged entry's source key
+  const uint32_t s = ki ? p.key_end[ki - 1] : 0u, e = p.key_end[ki];
   if (e - s <= 8 || e < s) {  // y.go:98 AssertTruef(len(key) > 8)
     atomicOr(p.flags, 1u);
     return;

@@ -125,9 +125,16 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
   const uint64_t pidx = f + lane;
   const uint64_t pc = pidx - 1 < p.n - 1 ? pidx - 1 : p.n - 1;
   const uint32_t pk = pidx ? p.key_end[pc] : 0u, pv = pidx ? p.vs_end[pc] : 0u;
+  // gather mode: the source starts of the same entries (entry f + lane)
+  uint32_t psk = 0, psv = 0;
+  if (p.src) {
+    const uint32_t si = p.src[pidx < p.n ? pidx : p.n - 1];
+    psk = si ? p.src_key_end[si - 1] : 0u;
+    psv = si ? p.src_vs_end[si - 1] : 0u;
+  }
   for (uint64_t e0 = 0; e0 < m; e0 += (uint64_t)G * EPP) {
     uint32_t klen[G], vlen[G], pos[G], np[G], kp[G];
-    uint64_t ks[G], vs0[G];
+    uint64_t ks[G], vs0[G], sk[G], sv[G];  // sk / sv: where the bytes are read (gather mode)
     bool on[G];
     const bool shuffled = e0 + (uint64_t)G * EPP < kWave;
 #pragma unroll
@@ -142,11 +149,22 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
         ke = (uint32_t)__shfl((int)pk, rr + 1);
         vs0[i] = (uint32_t)__shfl((int)pv, rr);
         ve = (uint32_t)__shfl((int)pv, rr + 1);
+        sk[i] = (uint32_t)__shfl((int)psk, rr);
+        sv[i] = (uint32_t)__shfl((int)psv, rr);
       } else {
         ks[i] = key_start(p, e);
         vs0[i] = vs_start(p, e);
         ke = p.key_end[e];
         ve = p.vs_end[e];
+        if (p.src) {
+          const uint32_t si = p.src[e];
+          sk[i] = si ? p.src_key_end[si - 1] : 0u;
+          sv[i] = si ? p.src_vs_end[si - 1] : 0u;
+        }
+      }
+      if (!p.src) {
+        sk[i] = ks[i];
+        sv[i] = vs0[i];
       }
       const uint64_t kl64 = ke - ks[i], vl64 = ve - vs0[i];
       klen[i] = (uint32_t)kl64;
@@ -183,7 +201,7 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
     for (uint32_t i = 0; i < G; i++) {
       for (uint32_t q = j; q < np[i]; q += J) {  // one (non-divergent) copy per piece
         const bool key = q < kp[i];
-        copy_piece16(out + pos[i] + 10 + (key ? 0u : klen[i]), key ? p.keys + ks[i] : p.vs + vs0[i],
+        copy_piece16(out + pos[i] + 10 + (key ? 0u : klen[i]), key ? p.keys + sk[i] : p.vs + sv[i],
                   key ? klen[i] : vlen[i], key ? q : q - kp[i]);
       }
     }

@@ -72,6 +72,11 @@ struct EncodeParams {
   const uint32_t* tbl_blk;
   const uint64_t* tbl_out;
   uint32_t ntables;
+  // gather mode (src != nullptr): entry e's bytes are source entry src[e] of keys / vs, whose
+  // ends are src_key_end / src_vs_end; key_end / vs_end are the entries' own (merged) ends
+  const uint32_t* src;
+  const uint32_t* src_key_end;
+  const uint32_t* src_vs_end;
 };
 
 // Builder.ReachedCapacity table cut over a sorted entry stream (encode.hip)
@@ -199,6 +204,7 @@ struct BloomSeg {
 struct BloomTables {
   const uint8_t* keys;
   const uint32_t* key_end;
+  const uint32_t* src;  // gather mode: key i is key src[i] of keys / key_end
   uint64_t* scratch;
   uint8_t* out;
   uint32_t* flags;

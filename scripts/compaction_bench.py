@@ -5,7 +5,8 @@ table merged with the concatenated bottom tables), device-resident end to end:
   cut     the merged stream into output tables where Builder.ReachedCapacity(64 MiB) starts a
           new one (levels.go:265-271)
   encode  every output table (100-entry blocks, Builder.Add / finishBlock / blockIndex) in one
-          launch
+          launch, reading each entry's bytes from the decoded tables through the merge's source
+          index (GATHER=0: the merge writes merged key / value streams and the encoder reads them)
 Top keys are updates of every 8th bottom key (same key, new value): the merge drops 1/9 of its
 input.  HIP-event times (median of 5) per stage; the oracle merge (sstref_merge, 1 thread)
 timed on the host for the same runs; the merged keys/values checked against it.
@@ -100,8 +101,13 @@ def main():
         data, d_off, d_len, int(ln.max()), C.MODE_MATERIALIZE, bufs, data_len=data.numel()))
     blk_first = bufs.blk_first.cpu().numpy().view(np.uint32)
     run_first = torch.tensor([0, int(blk_first[first_blk[1]]), n_in], dtype=torch.int32, device=dev)
+    # gather (default): the merge writes the merged order only and the encoder / bloom read
+    # each entry's bytes from the decoded tables through src (one copy, as builder.Add makes);
+    # GATHER=0: the merge also writes merged key / value streams and the encoder reads those
+    gather = os.environ.get("GATHER", "1") != "0"
     t_merge, m = timed(torch, stream, lambda: codec.merge_device(
-        bufs.key_data, bufs.key_end, bufs.val_data, bufs.val_end, run_first, n_in))
+        bufs.key_data, bufs.key_end, bufs.val_data, bufs.val_end, run_first, n_in,
+        gather=not gather))
     r = m["result"].cpu().numpy()
     n_out, kb, vb = int(r[0]), int(r[1]), int(r[2])
 
@@ -114,12 +120,20 @@ def main():
     cut["ntables"] = ntab_out
     d_out = torch.empty(out_bytes + 16, dtype=torch.uint8, device=dev)
     fl = torch.zeros(4, dtype=torch.int32, device=dev)
-    t_enc, _ = timed(torch, stream, lambda: codec.encode_tables_device(
-        cut, mk, mke, mv, mve, kb, vb, d_out, fl))
+    if gather:
+        t_enc, _ = timed(torch, stream, lambda: codec.encode_tables_gather_device(
+            cut, bufs.key_data, bufs.key_end, bufs.val_data, bufs.val_end, m["src"], mke, mve,
+            kb, vb, d_out, fl))
+        bargs = (bufs.key_data, bufs.key_end, d_out)
+        bsrc = m["src"]
+    else:
+        t_enc, _ = timed(torch, stream, lambda: codec.encode_tables_device(
+            cut, mk, mke, mv, mve, kb, vb, d_out, fl))
+        bargs, bsrc = (mk, mke, d_out), None
     # Finish's bloom tails (complete .sst files); the host reads the cut's small arrays first
     bfl = torch.zeros(1, dtype=torch.int32, device=dev)
-    codec.bloom_tables_device(cut, mk, mke, d_out, bfl)  # warm-up (and sizes the scratch)
-    t_bloom, _ = timed(torch, stream, lambda: codec.bloom_tables_device(cut, mk, mke, d_out, bfl))
+    codec.bloom_tables_device(cut, *bargs, bfl, src=bsrc)  # warm-up (and sizes the scratch)
+    t_bloom, _ = timed(torch, stream, lambda: codec.bloom_tables_device(cut, *bargs, bfl, src=bsrc))
 
     # oracle merge on the host, and the check
     import oracle_ffi
@@ -143,7 +157,7 @@ def main():
         "input_gibs": round(in_bytes / ((t_dec + t_merge + t_cut + t_enc + t_bloom) / 1e3) /
                             (1 << 30), 2),
         "cpu_oracle_merge_ms": round(cpu_merge_s * 1e3, 1),
-        "merge_matches_oracle": bool(ok)}))
+        "merge_matches_oracle": bool(ok), "gather": gather}))
     codec.close()
 
 

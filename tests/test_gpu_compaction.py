@@ -1,7 +1,9 @@
 """Device-resident compaction ("decode + encode into full compaction"):
 the input tables of compactBuildTables (levels.go:239-298) decoded in one GPU batch, merged
 (lsmgpu_merge_runs_async), cut where Builder.ReachedCapacity starts a new table
-(lsmgpu_cut_tables_async) and encoded (lsmgpu_encode_tables_async).  Checked byte for byte
+(lsmgpu_cut_tables_async) and encoded (lsmgpu_encode_tables_async), or -- gather mode -- merged
+without its bytes and encoded straight from the decoded tables through the merge's source
+index (lsmgpu_encode_tables_gather_async / lsmgpu_bloom_tables_gather_async).  Checked byte for byte
 against the oracle: sstref_merge order, then the oracle Builder driven exactly like the Go loop
 (`if builder.ReachedCapacity(cap) { break }; builder.Add(key, value)`, levels.go:265-271)."""
 import ctypes
@@ -43,9 +45,10 @@ def _oracle_tables(oracle, keys, vss, cap, bloom=False):
     return out
 
 
+@pytest.mark.parametrize("gather", [False, True])
 @pytest.mark.parametrize("bloom", [False, True])
 @pytest.mark.parametrize("cap", [1 << 17, 1 << 20, 3 << 20])  # 1 << 17: > 32 tables
-def test_device_compaction(codec, oracle, cap, bloom):
+def test_device_compaction(codec, oracle, cap, bloom, gather):
     import torch
     from lsmdb_amd import workload
     parts = []
@@ -72,14 +75,27 @@ def test_device_compaction(codec, oracle, cap, bloom):
     # device: merge -> cut -> encode, all on the device buffers
     dev = torch.device("cuda", codec.device)
     t = lambda a, dt: torch.from_numpy(np.array(a, copy=True).view(dt)).to(dev)
-    m = codec.merge_device(t(np.frombuffer(kd + b"\0" * 16, np.uint8), np.uint8),
-                           t(ke, np.int32), t(np.frombuffer(vd + b"\0" * 16, np.uint8), np.uint8),
-                           t(ve, np.int32), t(rf, np.int32), int(rf[-1]))
+    d_kd, d_ke = t(np.frombuffer(kd + b"\0" * 16, np.uint8), np.uint8), t(ke, np.int32)
+    d_vd, d_ve = t(np.frombuffer(vd + b"\0" * 16, np.uint8), np.uint8), t(ve, np.int32)
+    m = codec.merge_device(d_kd, d_ke, d_vd, d_ve, t(rf, np.int32), int(rf[-1]), gather=not gather)
     codec.synchronize()
     r = m["result"].cpu().numpy()
     n_out, kb, vb = int(r[0]), int(r[1]), int(r[2])
-    o = codec.compact_tables_device(m["key_data"], m["key_end"], m["val_data"], m["val_end"],
-                                    n_out, kb, vb, cap, bloom=bloom)
+    if not gather:
+        o = codec.compact_tables_device(m["key_data"], m["key_end"], m["val_data"], m["val_end"],
+                                        n_out, kb, vb, cap, bloom=bloom)
+    else:  # the merged order only; bytes read from the decoded tables through src
+        o = codec.cut_tables_device(m["key_end"], m["val_end"], n_out, cap, bloom=bloom)
+        codec.synchronize()
+        cr = o["result"].cpu().numpy()
+        o["ntables"], o["bytes"] = int(cr[0]), int(cr[2])
+        o["out"] = torch.empty(o["bytes"] + 16, dtype=torch.uint8, device=dev)
+        o["flags"] = torch.zeros(4, dtype=torch.int32, device=dev)
+        codec.encode_tables_gather_device(o, d_kd, d_ke, d_vd, d_ve, m["src"], m["key_end"],
+                                          m["val_end"], kb, vb, o["out"], o["flags"])
+        if bloom:
+            o["bloom_flags"] = torch.zeros(1, dtype=torch.int32, device=dev)
+            codec.bloom_tables_device(o, d_kd, d_ke, o["out"], o["bloom_flags"], src=m["src"])
     codec.synchronize()
     assert int(o["flags"][0].item()) == 0
     if bloom:
