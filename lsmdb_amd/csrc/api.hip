@@ -309,8 +309,6 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     const char* j_env = getenv("LSMGPU_WSC_J");  // A/B: lanes per entry in the copy
     p.wj = j_env ? (uint32_t)atoi(j_env) : 0u;
     if (p.wj != 8 && p.wj != 16) p.wj = 0;
-    const char* st_env = getenv("LSMGPU_WSC_STAGE");  // A/B: copy from an LDS copy of the block
-    p.wstage = st_env ? (uint32_t)atoi(st_env) : 0u;
     // view-only decode finishes inside the walk when there are >= 2 walk tiles (256 blocks)
     // per CU; with fewer, the tile epilogues run on too few workgroups and the copy launch wins
     // (measured: C2 1 GiB 0.413 -> 0.323 ms fused; C4 64 MiB, 21 tiles: 0.085 -> 0.165 ms).

@@ -488,33 +488,7 @@ __device__ __forceinline__ void copy_entries(const DecodeParams& p, const uint2*
 }
 
 // K2: one wave per block (p.wsplit waves above 8 KiB).
-constexpr uint32_t kCopyStage = 4096 + 32;  // one wave's staged block (+ alignment slack)
-constexpr uint32_t kCopyOut = 4096 + 64;    // one wave's staged output: values, then keys
-
-// One block's output stream [g0, g0 + len) from its LDS image (lds[h + x] = byte x, h = g0 & 15):
-// whole 16-B chunks as aligned 16-B stores, the two edge chunks (shared with the neighbouring
-// blocks' streams) byte by byte.
-__device__ __forceinline__ void flush_stream(uint8_t* g, uint64_t g0, uint32_t len,
-                                             const uint8_t* lds, uint32_t lane) {
-  const uint32_t h = (uint32_t)(g0 & 15u), nch = (h + len + 15) / 16;
-  uint8_t* ga = g + (g0 - h);
-  for (uint32_t c = lane; c < nch; c += kWave) {
-    const uint32_t lo = c == 0 ? h : 0u, hi = c == nch - 1 ? h + len - 16 * c : 16u;
-    if (lo == 0 && hi == 16) {
-      *reinterpret_cast<uint4*>(ga + 16 * c) = *reinterpret_cast<const uint4*>(lds + 16 * c);
-    } else {
-      for (uint32_t i = lo; i < hi; i++) ga[16 * c + i] = lds[16 * c + i];
-    }
-  }
-}
-
-// STAGE bit 1: the block's lines are loaded aligned and whole into LDS and the pieces read from
-// there; bit 2: the pieces are assembled in LDS and the key / value streams leave as aligned
-// 16-B stores (blocks <= 4 KiB, one wave per block; others take the global path)
-template <uint32_t STAGE>
 __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_blk[4][(STAGE & 1) ? kCopyStage : 16];
-  __shared__ __attribute__((aligned(16))) uint8_t s_out[4][(STAGE & 2) ? kCopyOut : 16];
   const uint32_t lane = lane_id();
   // p.wsplit waves share a block (large blocks): wave `sub` takes passes sub, sub + wsplit, ...
   const uint32_t wave = threadIdx.x >> 6, split = p.wsplit;
@@ -561,58 +535,6 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   }
   if (n == 0 || (p.ablate & 2)) return;
   const uint8_t* blk = p.data + off;
-  const uint32_t len = uniform(p.blk_len[b]);
-  const uint64_t a0 = off & ~15ull;
-  const uint32_t nst = (uint32_t)(((off + len + 15) & ~15ull) - a0);
-  if (STAGE && split == 1 && nst <= kCopyStage && mat) {
-    const uint8_t* sb = blk;
-    if constexpr ((STAGE & 1) != 0) {
-      // the block's lines, loaded aligned and whole (coalesced 16-B loads); the last chunk
-      // stops at the input buffer's end
-      uint8_t* st = s_blk[threadIdx.x >> 6];
-      for (uint32_t c = lane; c < nst / 16; c += kWave) {
-        const uint64_t ga = a0 + 16ull * c;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (ga + 16 <= p.data_len) {
-          v = *reinterpret_cast<const uint4*>(p.data + ga);
-        } else {
-          uint8_t t[16] = {};
-          for (uint32_t i = 0; i < 16 && ga + i < p.data_len; i++) t[i] = p.data[ga + i];
-          __builtin_memcpy(&v, t, 16);
-        }
-        *reinterpret_cast<uint4*>(st + 16 * c) = v;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      sb = st + (off - a0);
-    }
-    uint8_t* kb = p.key_data ? p.key_data + ek : nullptr;
-    uint8_t* vb = p.val_data ? p.val_data + ev : nullptr;
-    uint8_t* so = nullptr;
-    const uint32_t koff = (((uint32_t)(ev & 15u)) + V + 15u) & ~15u;
-    // values at so[ev & 15 ...], keys 16-B aligned after them; prefix-compressed keys can
-    // decode to more bytes than the block holds: those blocks write the streams directly
-    const bool ostage = (STAGE & 2) != 0 && koff + (uint32_t)(ek & 15u) + K <= kCopyOut;
-    if (ostage) {
-      so = s_out[threadIdx.x >> 6];
-      if (vb) vb = so + (ev & 15u);
-      if (kb) kb = so + koff + (ek & 15u);
-    }
-    const uint32_t avg = (K + V) / n;
-    if (p.wj == 16 || (p.wj == 0 && avg > 128))
-      copy_entries<16, 2>(p, meta, sb, kb, vb, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
-    else
-      copy_entries<8, 5>(p, meta, sb, kb, vb, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
-    if (ostage) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (p.val_data) flush_stream(p.val_data, ev, V, so, lane);
-      if (p.key_data) flush_stream(p.key_data, ek, K, so + koff, lane);
-    }
-    return;
-  }
   uint8_t* kbase = p.key_data ? p.key_data + ek : nullptr;
   uint8_t* vbase = p.val_data ? p.val_data + ev : nullptr;
   // lanes per entry from this block's average entry (known after the walk): 8 for C2-like
@@ -643,15 +565,7 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
   if (e == hipSuccess && mid) e = hipEventRecord(mid, s);
   if (e != hipSuccess || p.wfuse) return e;  // view-only: the walk wrote everything
   const uint32_t per_wg = 4 / p.wsplit;  // blocks per 4-wave workgroup
-  const dim3 cg((nblk + per_wg - 1) / per_wg);
-  if (p.wstage == 1)
-    hipLaunchKernelGGL(wsc_copy_kernel<1>, cg, dim3(256), 0, s, p);
-  else if (p.wstage == 2)
-    hipLaunchKernelGGL(wsc_copy_kernel<2>, cg, dim3(256), 0, s, p);
-  else if (p.wstage == 3)
-    hipLaunchKernelGGL(wsc_copy_kernel<3>, cg, dim3(256), 0, s, p);
-  else
-    hipLaunchKernelGGL(wsc_copy_kernel<0>, cg, dim3(256), 0, s, p);
+  hipLaunchKernelGGL(wsc_copy_kernel, dim3((nblk + per_wg - 1) / per_wg), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 

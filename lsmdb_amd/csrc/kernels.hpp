@@ -44,7 +44,6 @@ struct DecodeParams {
   uint32_t* wstatus;
   uint32_t wsplit;          // walk-scan-copy: waves per block in the copy (1, 2 or 4)
   uint32_t wj;              // walk-scan-copy: lanes per entry forced (8, 16), 0 = per block
-  uint32_t wstage;          // walk-scan-copy copy: stage blocks <= 4 KiB in LDS (aligned loads)
   uint32_t wfuse;           // walk-scan-copy, view-only mode: the walk writes the view index
                             // and per-block outputs itself (no copy launch)
   uint32_t wwalk;           // walk-scan-copy walk: kWalkLane / kWalkGroup (+ wlanes)

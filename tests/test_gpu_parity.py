@@ -547,15 +547,12 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     _assert_same(codec.decode_host(tight, so, sl_), oracle.decode(tight, so, sl_), "tight end")
 
 
-@pytest.mark.parametrize("stage", ["0", "1", "2", "3"])
-def test_wsc_mixed_copy(codec, oracle, monkeypatch, stage):
+def test_wsc_mixed_copy(codec, oracle, monkeypatch):
     """Walk-scan-copy's copy over every entry shape in one batch: C2 / C3 blocks, random key
     and value lengths with zero-length values, > 128 entries per block, prefix-compressed KAT
     blocks, 32 KiB C5 blocks, blocks at odd offsets, and the last block ending at the buffer's
-    end; pieces read from global memory or (stage 1, 3) from the block staged in LDS, written
-    straight to the streams or (stage 2, 3) assembled in LDS and stored as aligned chunks."""
+    end."""
     monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
-    monkeypatch.setenv("LSMGPU_WSC_STAGE", stage)
     c2 = _cols(2, 30000, seed=31)
     c3 = _cols(3, 2000, seed=32)
     c5 = _cols(5, 3000, seed=33)
