@@ -328,12 +328,6 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     if (wk_env && wk_env[0] == 'l') {
       p.wwalk = kWalkLane;
       p.wlanes = 1;
-    } else if (wk_env && strncmp(wk_env, "scan", 4) == 0) {
-      // "scan" / "scan4" / "scan16" / "scan64": blocks per tile (default by batch size)
-      const int t = atoi(wk_env + 4);
-      p.wwalk = kWalkScan;
-      p.wlanes = t == 4 || t == 16 || t == 64 ? (uint32_t)t
-                 : nblk <= 64ull * (uint64_t)c->num_cus ? 16u : 64u;
     } else if (wk_env && strncmp(wk_env, "group", 5) == 0) {
       const int l = atoi(wk_env + 5);  // "group" alone: 8 lanes
       p.wwalk = kWalkGroup;
@@ -342,22 +336,13 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     // d_result is zeroed by the walk kernel when a copy launch follows it (the copy's atomics
     // come after the kernel boundary): one operation fewer per decode.  A view-only decode
     // that ends in the walk updates d_result from every workgroup, so it is zeroed first.
-    // the scan walk loads a block in groups of 4 / 8 / 16 KiB
-    p.wchunks = max_blk_len <= 4096 ? 4u : 16u;
-    // the group walk first touches its blocks' lines, coalesced (LSMGPU_WSC_PREFETCH=0/1)
-    const char* pf_env = getenv("LSMGPU_WSC_PREFETCH");
-    p.wprefetch = p.wwalk == kWalkGroup && (pf_env ? atoi(pf_env) != 0 : false);
-    // the scan walk copies its blocks itself (LSMGPU_WSC_SCANCOPY=0: a copy launch follows)
-    const char* sc_env = getenv("LSMGPU_WSC_SCANCOPY");
-    p.wcopy = p.wwalk == kWalkScan && !(sc_env && atoi(sc_env) == 0);
-    if (p.wcopy) p.wfuse = 0;
-    if (p.wfuse || p.wcopy) HIPC(hipMemsetAsync(d_result, 0, 8 * sizeof(uint64_t), c->stream));
+    if (p.wfuse) HIPC(hipMemsetAsync(d_result, 0, 8 * sizeof(uint64_t), c->stream));
     else p.zero_result = 1;
     if (c->ktime) HIPC(hipEventRecord(c->kev[0], c->stream));
     HIPC(launch_decode_wsc(p, c->stream, c->ktime ? c->kev[1] : nullptr));
     if (c->ktime) HIPC(hipEventRecord(c->kev[2], c->stream));
     c->kvalid = c->ktime;
-    c->kfused = p.wfuse != 0 || p.wcopy != 0;
+    c->kfused = p.wfuse != 0;
     return LSMGPU_OK;
   }
   uint64_t waves = 0;

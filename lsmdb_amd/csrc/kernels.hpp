@@ -47,13 +47,8 @@ struct DecodeParams {
   uint32_t wfuse;           // walk-scan-copy, view-only mode: the walk writes the view index
                             // and per-block outputs itself (no copy launch)
   uint32_t wwalk;           // walk-scan-copy walk: kWalkLane / kWalkGroup (+ wlanes)
-  uint32_t wlanes;          // kWalkGroup: lanes per block (4, 8 or 16); kWalkScan: blocks per
-                            // tile (4, 16, 64: one wave scans wlanes / 4 of them in turn)
+  uint32_t wlanes;          // kWalkGroup: lanes per block (4, 8 or 16)
   uint32_t zero_result;     // walk-scan-copy with a copy launch: the walk zeroes result[0..7]
-  uint32_t wchunks;         // kWalkScan: 1 KiB chunks loaded at once (4 for blocks <= 4 KiB, 16)
-  uint32_t wprefetch;       // kWalkGroup: touch the wave's blocks' lines before the walk
-  uint32_t wcopy;           // kWalkScan: each walk workgroup copies its own blocks after its
-                            // look-back (no copy launch; result zeroed before the launch)
 };
 
 // Encode: one wave per output block; every byte position is closed-form
@@ -226,7 +221,6 @@ hipError_t launch_bloom_json(const BloomJson& p, hipStream_t s);
 // walk-scan-copy walk modes (DecodeParams::wwalk)
 constexpr int kWalkLane = 0;    // one lane per block, header by header from HBM
 constexpr int kWalkGroup = 2;   // wlanes lanes per block, speculative same-shape runs from HBM
-constexpr int kWalkScan = 3;    // one wave per block: data-parallel header candidates + chain check
 // which decode path a batch takes: 0 register-lag (<= 4 KiB), 1 LDS-lag, 2 walk-scan-copy
 // (blocks < 64 KiB, batches of >= kWscMinBlocks blocks)
 constexpr uint32_t kWscMinBlocks = 1024;

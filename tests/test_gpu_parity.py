@@ -499,18 +499,17 @@ def test_wsc_lanes_per_entry(codec, oracle, monkeypatch, lanes):
     _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln), f"J={lanes}")
 
 
-@pytest.mark.parametrize("walk", ["lane", "group", "group2", "group4", "group16", "scan", "scan0"])
+@pytest.mark.parametrize("walk", ["lane", "group", "group2", "group4", "group16"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
-    """Walk-scan-copy's walks (LSMGPU_WSC_WALK): one lane per block from HBM, 8 / 4 / 16
-    lanes per block guessing same-shape runs from HBM, or one wave per block finding the
-    headers by a data-parallel candidate scan.  C2 / C3 / C4 (100 entries per block) blocks, short and tiny entries (> 64 per block), every KAT block (error statuses,
+    """Walk-scan-copy's walks (LSMGPU_WSC_WALK): one lane per block from HBM, or 8 / 4
+    / 16 lanes per block guessing same-shape runs from HBM.  C2 / C3 / C4 (100 entries
+    per block) blocks, short and tiny entries (> 64 per block), every KAT block (error statuses,
     terminators, plen > 0) at odd alignments, prefix-compressed random blocks, a ragged last
     tile and a block ending at the buffer's end (plus C5 32 KiB blocks for the HBM walks)."""
     from lsmdb_amd.codec import MODE_MATERIALIZE, MODE_VIEW
     monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
-    monkeypatch.setenv("LSMGPU_WSC_WALK", walk.rstrip("0"))
-    monkeypatch.setenv("LSMGPU_WSC_SCANCOPY", "0" if walk == "scan0" else "1")  # scan0: copy launch
+    monkeypatch.setenv("LSMGPU_WSC_WALK", walk)
     monkeypatch.setenv("LSMGPU_WSC_VIEWFUSE", "1")
     c2 = _cols(2, 40000, seed=23)
     c3 = _cols(3, 3000, seed=24)
@@ -596,7 +595,7 @@ def _block_entries(block):
     return out
 
 
-@pytest.mark.parametrize("walk", ["lane", "group", "scan", "scan0"])
+@pytest.mark.parametrize("walk", ["lane", "group"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
     """Blocks built to defeat a header-pattern filter, decoded by every walk.  Keys and
@@ -608,8 +607,7 @@ def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
     oracle's iterator does."""
     from lsmdb_amd.codec import MODE_MATERIALIZE, MODE_VIEW
     monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
-    monkeypatch.setenv("LSMGPU_WSC_WALK", walk.rstrip("0"))
-    monkeypatch.setenv("LSMGPU_WSC_SCANCOPY", "0" if walk == "scan0" else "1")  # scan0: copy launch
+    monkeypatch.setenv("LSMGPU_WSC_WALK", walk)
     monkeypatch.setenv("LSMGPU_WSC_VIEWFUSE", "1")
     rng = np.random.default_rng(77)
     parts = []
