@@ -129,8 +129,9 @@ __device__ __forceinline__ WalkResult walk_meta(const Src& src, const uint8_t* f
 // ticket makes every predecessor tile already running, so the look-back always progresses.
 // MODE kWalkGroup (p.wwalk, the default when nblk <= 64 per CU: the lane walk would leave the
 // machine idle): 256 / TB lanes per block guess same-shape runs (see the branch).
-// MODE kWalkLane: lane b walks block b straight from HBM, one dependent 8-B header load per
-// entry (every 128-B line of the input is fetched on its own, as scattered requests).
+// MODE kWalkLane: lane b walks block b straight from HBM, one dependent 8-B non-temporal header
+// load per entry (every 128-B line of the input is fetched on its own, as scattered requests);
+// the records leave in whole 128-B lines written by 8 lanes each.
 template <int MODE, uint32_t TB>  // TB = blocks per tile (<= 256 threads: thread t owns block t)
 __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   static_assert(TB <= 256, "one thread per block of the tile");
@@ -274,41 +275,77 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
       t[2] = V;
       p.wstatus[b] = st;
     }
-  } else if (b < p.nblk) {
+  } else {
+    // Lane walk, records flushed cooperatively: every lane walks in lockstep (a lane that
+    // stopped idles), so after iteration k with k % 16 == 15 every lane still walking holds
+    // records k-15 .. k in its LDS row; the wave then writes those rows as whole 128-B lines,
+    // 8 lanes per line -- 8 lines per store instruction instead of 64 partial ones (C2 1 GiB,
+    // same box: walk 0.233 -> 0.222 ms, view decode 0.271 -> 0.261 ms).
+    const bool valid = b < p.nblk;
     uint2* row = stage + tid * kWalkStage;
-    const uint32_t off = p.blk_off[b], len = p.blk_len[b];
-    uint32_t pos = 0;
-    s_off[tid] = off;
-    uint2* meta = reinterpret_cast<uint2*>(p.wmeta) + (uint64_t)b * p.wcap;
-    if ((uint64_t)off + len > p.data_len) {
+    uint32_t off = 0, len = 0, pos = 0;
+    if (valid) {
+      off = p.blk_off[b];
+      len = p.blk_len[b];
+      s_off[tid] = off;
+    }
+    bool done = !valid;
+    if (valid && (uint64_t)off + len > p.data_len) {
       st = LSMGPU_BLK_RANGE;
-    } else {
-      const uint8_t* blk = p.data + off;
-      for (;;) {
-        if (pos >= len) break;                                   // iterator.go:115-118
-        if (len - pos < 10) { st = LSMGPU_BLK_TRUNC_HEADER; break; }
-        uint32_t plen, klen, vlen;
-        read_hdr_nt(blk + pos, plen, klen, vlen);                // iterator.go:121
-        if ((klen | plen) == 0) break;                           // iterator.go:124-127
-        if (n == 0 && plen != 0) { st = LSMGPU_BLK_FIRST_PLEN; break; }  // iterator.go:129-133
-        if (10 + plen > len) { st = LSMGPU_BLK_PREFIX_OOB; break; }      // base key = entry 0's
-        const uint32_t end = pos + 10 + klen + vlen;             // iterator.go:101-109
-        if (end > len) { st = LSMGPU_BLK_VALUE_OVERFLOW; break; }
-        row[n & 15] = make_uint2(pos | (V << 16), K);  // n < wcap - 1: >= 10 B per entry
-        if ((n & 15) == 15) flush_meta(meta + (n - 15), row, 16);
-        K += plen + klen;
-        V += vlen;
-        n++;
-        pos = end;
+      done = true;
+    }
+    const uint8_t* blk = p.data + off;
+    const uint32_t wb0 = tile * 256 + wave * 64;  // the block of this wave's lane 0
+    for (uint32_t k = 0;; k++) {
+      if (__ballot(!done) == 0) break;
+      bool rec = false;
+      if (!done) {
+        do {
+          if (pos >= len) { done = true; break; }                  // iterator.go:115-118
+          if (len - pos < 10) { st = LSMGPU_BLK_TRUNC_HEADER; done = true; break; }
+          uint32_t plen, klen, vlen;
+          read_hdr_nt(blk + pos, plen, klen, vlen);                // iterator.go:121
+          if ((klen | plen) == 0) { done = true; break; }          // iterator.go:124-127
+          if (n == 0 && plen != 0) { st = LSMGPU_BLK_FIRST_PLEN; done = true; break; }
+          if (10 + plen > len) { st = LSMGPU_BLK_PREFIX_OOB; done = true; break; }
+          const uint32_t end = pos + 10 + klen + vlen;             // iterator.go:101-109
+          if (end > len) { st = LSMGPU_BLK_VALUE_OVERFLOW; done = true; break; }
+          row[n & 15] = make_uint2(pos | (V << 16), K);
+          K += plen + klen;
+          V += vlen;
+          n++;
+          pos = end;
+          rec = true;
+        } while (false);
+      }
+      if ((k & 15) == 15) {
+        const uint64_t fl = __ballot(rec);  // lanes holding records k-15 .. k
+        if (fl) {
+          wave_lds_fence();
+#pragma unroll
+          for (uint32_t r = 0; r < 8; r++) {
+            const uint32_t L = 8 * r + (lane >> 3), part = lane & 7;
+            if ((fl >> L) & 1ull) {
+              const uint2* rw = stage + (wave * 64 + L) * kWalkStage + 2 * part;
+              const uint2 a = rw[0], c = rw[1];
+              uint2* mL = reinterpret_cast<uint2*>(p.wmeta) + (uint64_t)(wb0 + L) * p.wcap + (k - 15);
+              reinterpret_cast<uint4*>(mL)[part] = make_uint4(a.x, a.y, c.x, c.y);
+            }
+          }
+          wave_lds_fence();
+        }
       }
     }
-    row[n & 15] = make_uint2(pos | (V << 16), K);
-    flush_meta(meta + (n & ~15u), row, (n & 15) + 1);
-    uint64_t* t = p.wstat + 3ull * b;
-    t[0] = n;
-    t[1] = K;
-    t[2] = V;
-    p.wstatus[b] = st;
+    if (valid) {
+      uint2* meta = reinterpret_cast<uint2*>(p.wmeta) + (uint64_t)b * p.wcap;
+      row[n & 15] = make_uint2(pos | (V << 16), K);
+      flush_meta(meta + (n & ~15u), row, (n & 15) + 1);
+      uint64_t* t = p.wstat + 3ull * b;
+      t[0] = n;
+      t[1] = K;
+      t[2] = V;
+      p.wstatus[b] = st;
+    }
   }
   // tile scan (saturating u32: a key stream past 4 GiB - 1 fails the copy's capacity check)
   const uint32_t in_ = wave_scan_sat(n, lane), ik = wave_scan_sat(K, lane),
