@@ -283,9 +283,10 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
   p.tag = c->tag;
   int path = decode_path(max_blk_len, (uint32_t)nblk);
   if (path == 2) {  // walk-scan-copy: blocks of 4 KiB .. 64 KiB - 1
-    // entries of a block (>= 10 B each) + the sentinel, rounded to 16-entry (128-B) chunks
-    const uint32_t cap = (max_blk_len / 10 + 1 + 15) / 16 * 16;
-    const size_t meta_b = (size_t)nblk * cap * 8;
+    // entries of a block (>= 10 B each) + the sentinel, 4-B records rounded to 32-record
+    // (128-B) chunks
+    const uint32_t cap = (max_blk_len / 10 + 1 + 31) / 32 * 32;
+    const size_t meta_b = (size_t)nblk * cap * 4;
     const size_t tri_b = ((size_t)nblk * 24 + 255) / 256 * 256;
     const size_t wneed = meta_b + 2 * tri_b + (size_t)nblk * 4;
     if (wneed > c->wsc.cap) {

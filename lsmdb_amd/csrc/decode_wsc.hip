@@ -5,8 +5,8 @@
 // blocks per wave, every block of the batch in flight, each hop one dependent 8-B load -- and
 // the bytes are then moved by a separate, fully parallel copy with known output bases:
 //   K1 walk_kernel : lane b walks block b exactly like blockIterator.Next/parseKV
-//                    (table/iterator.go:93-135), writing per entry {pos | value offset << 16,
-//                    key offset} (full-line chunks, see flush_meta) and {entries, key
+//                    (table/iterator.go:93-135), writing per entry a 4-B record {pos | value
+//                    offset << 16} (full-line chunks, see flush_meta) and {entries, key
 //                    bytes, value bytes} + status per block; each 256-block workgroup then
 //                    scans its blocks and finds its base by decoupled look-back, so K1 ends
 //                    with every block's output base
@@ -53,72 +53,26 @@ __device__ __forceinline__ void read_hdr_nt(const uint8_t* g, uint32_t& plen, ui
 
 }  // namespace
 
-// Per-entry metadata of the walk: uint2 {header pos | value offset << 16, key offset} (key
-// offsets count plen + stored bytes: u32, prefix-compressed blocks may pass 64 KiB), entry n
-// = the sentinel {stop pos | V << 16, K}.  Block b's entries are contiguous at b * wcap
-// (wcap a multiple of 16: 128-B aligned chunks of 16 entries).  The walking lane stages 16
-// entries in LDS and writes each chunk as one full 128-B line -- 8-B stores straight from
-// 64 lanes at 64 different blocks were evicted from L2 as partial lines (4x the bytes).
-constexpr uint32_t kWalkStage = 17;  // uint2 per lane row: 16 entries + 1 pad (bank spread)
+// Per-entry metadata of the walk: one u32 record {header pos | value offset << 16} per entry
+// (both < 64 KiB in a block < 64 KiB), entry n = the sentinel {stop pos | V << 16}.  The copy
+// derives the rest: value length = the next record's value offset minus this one's, stored key
+// length = the next header position - this one - 10 - the value length, and (no entry with
+// plen > 0, i.e. every block Builder writes) the key offset = pos - 10 e - value offset;
+// a block whose K differs from that sum has plen > 0 entries and takes a header-reading path.
+// Block b's records are contiguous at b * wcap (wcap a multiple of 32: 128-B aligned chunks of 32
+// records).  The walk stages 32 records per block in LDS and writes each chunk as one full
+// 128-B line -- 8-B stores straight from 64 lanes at 64 different blocks were evicted from L2 as
+// partial lines (4x the bytes).  Round 3: 4-B records instead of {pos | V << 16, K} (8 B).
+constexpr uint32_t kWalkStage = 33;  // u32 per lane row: 32 records + 1 pad (bank spread)
 
-__device__ __forceinline__ void flush_meta(uint2* dst, const uint2* row, uint32_t cnt) {
-  if (cnt == 16) {
+__device__ __forceinline__ void flush_meta(uint32_t* dst, const uint32_t* row, uint32_t cnt) {
+  if (cnt == 32) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      uint4 v;
-      v.x = row[2 * i].x;
-      v.y = row[2 * i].y;
-      v.z = row[2 * i + 1].x;
-      v.w = row[2 * i + 1].y;
-      reinterpret_cast<uint4*>(dst)[i] = v;
-    }
+    for (int i = 0; i < 8; i++)
+      reinterpret_cast<uint4*>(dst)[i] = make_uint4(row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3]);
   } else {
     for (uint32_t i = 0; i < cnt; i++) dst[i] = row[i];
   }
-}
-
-// One block's walk (blockIterator.Next/parseKV, table/iterator.go:93-135) over `src` (LDS slot
-// or global bytes), writing the metadata records {header pos | value offset << 16, key offset}
-// + the sentinel straight to `meta`.  A fast loop takes plen == 0 entries (all Builder writes,
-// SURVEY F1) with one 8-B header read each; the general loop continues from wherever it stops
-// and applies every stop rule in the iterator's order.
-template <class Src>
-__device__ __forceinline__ WalkResult walk_meta(const Src& src, const uint8_t* fast, uint32_t len,
-                                                uint2* meta) {
-  uint32_t pos = 0, n = 0, K = 0, V = 0, st = LSMGPU_BLK_OK;
-  if (fast) {
-    for (;;) {
-      uint2 hw;
-      __builtin_memcpy(&hw, fast + pos, 8);  // pos <= len keeps the read inside the block's span
-      const uint32_t plen = __builtin_amdgcn_perm(0u, hw.x, 0x0c0c0001u);
-      const uint32_t klen = __builtin_amdgcn_perm(0u, hw.x, 0x0c0c0203u);
-      const uint32_t vlen = __builtin_amdgcn_perm(0u, hw.y, 0x0c0c0001u);
-      const uint32_t end = pos + 10 + klen + vlen;
-      if ((len - pos < 10) | (klen == 0) | (plen != 0) | (end > len)) break;
-      meta[n] = make_uint2(pos | (V << 16), K);
-      K += klen;
-      V += vlen;
-      n++;
-      pos = end;
-    }
-  }
-  for (;;) {
-    if (pos >= len) break;                                   // iterator.go:115-118
-    if (len - pos < 10) { st = LSMGPU_BLK_TRUNC_HEADER; break; }
-    const Hdr h = src.hdr(pos);                              // iterator.go:121
-    if ((h.klen | h.plen) == 0) break;                       // iterator.go:124-127
-    if (n == 0 && h.plen != 0) { st = LSMGPU_BLK_FIRST_PLEN; break; }  // iterator.go:129-133
-    if (10 + h.plen > len) { st = LSMGPU_BLK_PREFIX_OOB; break; }      // base key = entry 0's
-    const uint32_t end = pos + 10 + h.klen + h.vlen;         // iterator.go:101-109
-    if (end > len) { st = LSMGPU_BLK_VALUE_OVERFLOW; break; }
-    meta[n] = make_uint2(pos | (V << 16), K);
-    K += h.plen + h.klen;
-    V += h.vlen;
-    n++;
-    pos = end;
-  }
-  meta[n] = make_uint2(pos | (V << 16), K);  // sentinel
-  return WalkResult{n, K, V, st};
 }
 
 // K1: lane = block; a workgroup = a tile of 256 consecutive blocks, tiles taken in ticket order
@@ -135,14 +89,14 @@ __device__ __forceinline__ WalkResult walk_meta(const Src& src, const uint8_t* f
 template <int MODE, uint32_t TB>  // TB = blocks per tile (<= 256 threads: thread t owns block t)
 __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   static_assert(TB <= 256, "one thread per block of the tile");
-  constexpr uint32_t kStageBytes = 256 * kWalkStage * sizeof(uint2);
+  constexpr uint32_t kStageBytes = 256 * kWalkStage * sizeof(uint32_t);
   // group walk: a 32-record ring per block (the walk's LDS also serves the view epilogue's
   // owner map)
-  constexpr uint32_t kLdsBytes = MODE == kWalkGroup ? TB * 16 * sizeof(uint2) : kStageBytes;
+  constexpr uint32_t kLdsBytes = MODE == kWalkGroup ? TB * 32 * sizeof(uint32_t) : kStageBytes;
   static_assert(MODE != kWalkLane || kLdsBytes == kStageBytes,
-                "the lane walk stages 16 records per lane");
+                "the lane walk stages 32 records per lane");
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
-  uint2* const stage = reinterpret_cast<uint2*>(lds);
+  uint32_t* const stage = reinterpret_cast<uint32_t*>(lds);
   __shared__ uint32_t s_tile;
   __shared__ uint32_t s_wave[4][3];
   __shared__ uint32_t s_ex[3];
@@ -175,10 +129,10 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     constexpr uint32_t kGroupProbe = 16;
     const uint32_t g = tid / L, k = tid & (L - 1), gb = lane & ~(L - 1);
     const uint32_t bg = tile * TB + g;
-    uint2* row = stage + g * 16;  // the block's current 16-record chunk (one 128-B line)
+    uint32_t* row = stage + g * 32;  // the block's current 32-record chunk (one 128-B line)
     if (bg < p.nblk) {
       const uint32_t off = p.blk_off[bg], len = p.blk_len[bg];
-      uint2* meta = reinterpret_cast<uint2*>(p.wmeta) + (uint64_t)bg * p.wcap;
+      uint32_t* meta = p.wmeta + (uint64_t)bg * p.wcap;
       uint32_t pos = 0, gn = 0, gK = 0, gV = 0, gst = LSMGPU_BLK_OK;
       if ((uint64_t)off + len > p.data_len) {
         gst = LSMGPU_BLK_RANGE;
@@ -200,9 +154,9 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
           if (!(fb & 1u)) break;  // entry n itself needs the general loop (or the block ended)
           const uint32_t t = __builtin_ctz(~sb);                          // leading same-shape run
           const uint32_t m = t + ((t < L && ((fb >> t) & 1u)) ? 1u : 0u);  // + one new shape
-          const uint2 rec = make_uint2(q | ((gV + k * vref) << 16), gK + k * kref);
-          const uint32_t idx = gn + k, cend = (gn | 15u) + 1;  // end of the current chunk
-          if (k < m && idx < cend) row[idx & 15] = rec;
+          const uint32_t rec = q | ((gV + k * vref) << 16);
+          const uint32_t idx = gn + k, cend = (gn | 31u) + 1;  // end of the current chunk
+          if (k < m && idx < cend) row[idx & 31] = rec;
           const uint32_t src = gb + m - 1;  // the last accepted entry
           pos = (uint32_t)__shfl((int)endq, (int)src);
           const uint32_t shape = (uint32_t)__shfl((int)(klen | (vlen << 16)), (int)src);
@@ -218,14 +172,13 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
             stride = 10 + kref + vref;
           }
           rounds++;
-          if (gn >= cend) {  // chunk [cend - 16, cend) complete: one full 128-B line
+          if (gn >= cend) {  // chunk [cend - 32, cend) complete: one full 128-B line
             __builtin_amdgcn_wave_barrier();
-            for (uint32_t i = k; i < 8; i += L) {
-              const uint2 a = row[2 * i], c = row[2 * i + 1];
-              reinterpret_cast<uint4*>(meta + cend - 16)[i] = make_uint4(a.x, a.y, c.x, c.y);
-            }
+            for (uint32_t i = k; i < 8; i += L)
+              reinterpret_cast<uint4*>(meta + cend - 32)[i] =
+                  make_uint4(row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3]);
             __builtin_amdgcn_wave_barrier();  // the chunk is read before the next one fills
-            if (k < m && idx >= cend) row[idx & 15] = rec;
+            if (k < m && idx >= cend) row[idx & 31] = rec;
           }
           // shapes do not repeat in this block (< 1.25 entries per round after 16 rounds): the
           // rest entry by entry.  A rate over many rounds, not a streak -- with thousands of
@@ -244,8 +197,8 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
             if (10 + plen > len) { gst = LSMGPU_BLK_PREFIX_OOB; break; }
             const uint32_t end = pos + 10 + klen + vlen;             // iterator.go:101-109
             if (end > len) { gst = LSMGPU_BLK_VALUE_OVERFLOW; break; }
-            row[gn & 15] = make_uint2(pos | (gV << 16), gK);
-            if ((gn & 15) == 15) flush_meta(meta + (gn - 15), row, 16);
+            row[gn & 31] = pos | (gV << 16);
+            if ((gn & 31) == 31) flush_meta(meta + (gn - 31), row, 32);
             gK += plen + klen;
             gV += vlen;
             gn++;
@@ -254,8 +207,8 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
         }
       }
       if (k == 0) {
-        row[gn & 15] = make_uint2(pos | (gV << 16), gK);  // sentinel
-        flush_meta(meta + (gn & ~15u), row, (gn & 15) + 1);
+        row[gn & 31] = pos | (gV << 16);  // sentinel
+        flush_meta(meta + (gn & ~31u), row, (gn & 31) + 1);
         s_res[0][g] = gn;
         s_res[1][g] = gK;
         s_res[2][g] = gV;
@@ -277,12 +230,12 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     }
   } else {
     // Lane walk, records flushed cooperatively: every lane walks in lockstep (a lane that
-    // stopped idles), so after iteration k with k % 16 == 15 every lane still walking holds
-    // records k-15 .. k in its LDS row; the wave then writes those rows as whole 128-B lines,
+    // stopped idles), so after iteration k with k % 32 == 31 every lane still walking holds
+    // records k-31 .. k in its LDS row; the wave then writes those rows as whole 128-B lines,
     // 8 lanes per line -- 8 lines per store instruction instead of 64 partial ones (C2 1 GiB,
     // same box: walk 0.233 -> 0.222 ms, view decode 0.271 -> 0.261 ms).
     const bool valid = b < p.nblk;
-    uint2* row = stage + tid * kWalkStage;
+    uint32_t* row = stage + tid * kWalkStage;
     uint32_t off = 0, len = 0, pos = 0;
     if (valid) {
       off = p.blk_off[b];
@@ -310,7 +263,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
           if (10 + plen > len) { st = LSMGPU_BLK_PREFIX_OOB; done = true; break; }
           const uint32_t end = pos + 10 + klen + vlen;             // iterator.go:101-109
           if (end > len) { st = LSMGPU_BLK_VALUE_OVERFLOW; done = true; break; }
-          row[n & 15] = make_uint2(pos | (V << 16), K);
+          row[n & 31] = pos | (V << 16);
           K += plen + klen;
           V += vlen;
           n++;
@@ -318,18 +271,17 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
           rec = true;
         } while (false);
       }
-      if ((k & 15) == 15) {
-        const uint64_t fl = __ballot(rec);  // lanes holding records k-15 .. k
+      if ((k & 31) == 31) {
+        const uint64_t fl = __ballot(rec);  // lanes holding records k-31 .. k
         if (fl) {
           wave_lds_fence();
 #pragma unroll
           for (uint32_t r = 0; r < 8; r++) {
             const uint32_t L = 8 * r + (lane >> 3), part = lane & 7;
             if ((fl >> L) & 1ull) {
-              const uint2* rw = stage + (wave * 64 + L) * kWalkStage + 2 * part;
-              const uint2 a = rw[0], c = rw[1];
-              uint2* mL = reinterpret_cast<uint2*>(p.wmeta) + (uint64_t)(wb0 + L) * p.wcap + (k - 15);
-              reinterpret_cast<uint4*>(mL)[part] = make_uint4(a.x, a.y, c.x, c.y);
+              const uint32_t* rw = stage + (wave * 64 + L) * kWalkStage + 4 * part;
+              uint32_t* mL = p.wmeta + (uint64_t)(wb0 + L) * p.wcap + (k - 31);
+              reinterpret_cast<uint4*>(mL)[part] = make_uint4(rw[0], rw[1], rw[2], rw[3]);
             }
           }
           wave_lds_fence();
@@ -337,9 +289,9 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
       }
     }
     if (valid) {
-      uint2* meta = reinterpret_cast<uint2*>(p.wmeta) + (uint64_t)b * p.wcap;
-      row[n & 15] = make_uint2(pos | (V << 16), K);
-      flush_meta(meta + (n & ~15u), row, (n & 15) + 1);
+      uint32_t* meta = p.wmeta + (uint64_t)b * p.wcap;
+      row[n & 31] = pos | (V << 16);
+      flush_meta(meta + (n & ~31u), row, (n & 31) + 1);
       uint64_t* t = p.wstat + 3ull * b;
       t[0] = n;
       t[1] = K;
@@ -448,26 +400,26 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     const uint64_t bend = e0 + s_first[lo + 1];
     if (bend > p.ent_cap || bend > 0xffffffffull) continue;  // reported above (result[5])
     const uint32_t i = e - s_first[lo];
-    const uint2* meta = reinterpret_cast<const uint2*>(p.wmeta) + (uint64_t)(tile * TB + lo) * p.wcap;
-    const uint2 m0 = meta[i], m1 = meta[i + 1];
-    const uint32_t hp = m0.x & 0xffffu, vl = (m1.x >> 16) - (m0.x >> 16);
-    const uint32_t kl = (m1.x & 0xffffu) - hp - 10 - vl;  // stored key bytes
+    const uint32_t* meta = p.wmeta + (uint64_t)(tile * TB + lo) * p.wcap;
+    const uint32_t m0 = meta[i], m1 = meta[i + 1];
+    const uint32_t hp = m0 & 0xffffu, vl = (m1 >> 16) - (m0 >> 16);
+    const uint32_t kl = (m1 & 0xffffu) - hp - 10 - vl;  // stored key bytes
     p.view[e0 + e] = (uint64_t)(s_off[lo] + hp + 10) | ((uint64_t)kl << 32) | ((uint64_t)vl << 48);
   }
 }
 
-// The entries of one block: J lanes per entry; an entry's pieces are [key pieces | value
-// pieces] (16 B, the last overlapping back inside its stream, or two overlapping 8/4/2/1-B
-// pieces below 16 B) and lane j takes pieces j, j + J, ...  G entry groups per pass, all
-// metadata loads issued first.
+// The entries of one block with no prefix-compressed entry: J lanes per entry; an entry's
+// pieces are [key pieces | value pieces] (16 B, the last overlapping back inside its stream, or
+// two overlapping 8/4/2/1-B pieces below 16 B) and lane j takes pieces j, j + J, ...  G entry
+// groups per pass, all metadata loads issued first.  Key offset of entry e = pos - 10 e - value
+// offset (every earlier entry contributed its 10-B header, its stored key and its value).
 template <uint32_t J, uint32_t G>
-__device__ __forceinline__ void copy_entries(const DecodeParams& p, const uint2* meta,
+__device__ __forceinline__ void copy_entries(const DecodeParams& p, const uint32_t* meta,
                                              const uint8_t* blk, uint8_t* kbase, uint8_t* vbase,
                                              uint32_t n, uint64_t en, uint64_t ek, uint64_t ev,
                                              uint32_t off, uint32_t sub, uint32_t split,
-                                             bool mat, bool view, uint32_t lane, uint2 pre) {
+                                             bool mat, bool view, uint32_t lane, uint32_t pre) {
   const uint32_t j = lane & (J - 1);
-  bool any_plen = false;
   for (uint32_t e0 = sub * G * (kWave / J); e0 < n; e0 += split * G * (kWave / J)) {
     uint32_t hp[G], kl[G], vl[G], ko[G], vo[G], np[G], kp[G];
     bool on[G];
@@ -478,26 +430,23 @@ __device__ __forceinline__ void copy_entries(const DecodeParams& p, const uint2*
     for (int i = 0; i < G; i++) {
       const uint32_t e = e0 + i * (kWave / J) + (lane / J);
       const uint32_t ec = min(e, n - 1);
-      uint2 m0, m1;
+      uint32_t m0, m1;
       if (shuffled) {
-        m0.x = (uint32_t)__shfl((int)pre.x, (int)ec);
-        m0.y = (uint32_t)__shfl((int)pre.y, (int)ec);
-        m1.x = (uint32_t)__shfl((int)pre.x, (int)ec + 1);
-        m1.y = (uint32_t)__shfl((int)pre.y, (int)ec + 1);
+        m0 = (uint32_t)__shfl((int)pre, (int)ec);
+        m1 = (uint32_t)__shfl((int)pre, (int)ec + 1);
       } else {
         m0 = meta[ec];
         m1 = meta[ec + 1];
       }
-      hp[i] = m0.x & 0xffffu;
-      vo[i] = m0.x >> 16;
-      ko[i] = m0.y;
-      const uint32_t ko1 = m1.y, vo1 = m1.x >> 16;
+      hp[i] = m0 & 0xffffu;
+      vo[i] = m0 >> 16;
+      const uint32_t hp1 = m1 & 0xffffu, vo1 = m1 >> 16;
       vl[i] = vo1 - vo[i];
-      kl[i] = (m1.x & 0xffffu) - hp[i] - 10 - vl[i];  // stored key bytes
-      const uint32_t plen = ko1 - ko[i] - kl[i];
+      kl[i] = hp1 - hp[i] - 10 - vl[i];  // stored key bytes
+      ko[i] = hp[i] - 10 * ec - vo[i];
+      const uint32_t ko1 = ko[i] + kl[i];
       on[i] = e < n;
-      any_plen = any_plen || (on[i] && plen != 0);
-      kp[i] = plen ? 0u : pieces16(kl[i]);  // prefix-compressed keys: bytewise pass below
+      kp[i] = pieces16(kl[i]);
       np[i] = kp[i] + pieces16(vl[i]);
       if (on[i] && j == 0) {
         if (mat) {
@@ -523,20 +472,41 @@ __device__ __forceinline__ void copy_entries(const DecodeParams& p, const uint2*
       }
     }
   }
-  if (any_plen && kbase && mat) {  // baseKey[:plen] ++ diff (iterator.go:98-100): bytewise
-    // the same passes as above (any_plen covers only this wave's entries)
-    for (uint32_t e = sub * G * (kWave / J) + (lane / J); e < n;
-         e += ((e / (kWave / J)) % G == G - 1) ? (split - 1) * G * (kWave / J) + kWave / J
-                                              : kWave / J) {
-      const uint2 m0 = meta[e], m1 = meta[e + 1];
-      const uint32_t hp = m0.x & 0xffffu, ko = m0.y;
-      const uint32_t vl = (m1.x >> 16) - (m0.x >> 16);
-      const uint32_t kl = m1.y - ko;                                // output key bytes
-      const uint32_t plen = kl - ((m1.x & 0xffffu) - hp - 10 - vl);
-      if (plen == 0) continue;
-      for (uint32_t i = j; i < kl; i += J)
-        kbase[ko + i] = i < plen ? blk[10 + i] : blk[hp + 10 + i - plen];
+}
+
+// A block with prefix-compressed entries (plen > 0: never written by Builder; the
+// format the iterator accepts): entries 64 at a time, lane = entry, plen read from the header,
+// key offsets by a wave scan of plen + stored key bytes; keys bytewise as baseKey[:plen] ++ diff
+// (iterator.go:98-100), values as 16-B pieces.  Whole wave; `sub` / `split` share the entries.
+__device__ __forceinline__ void copy_entries_plen(const DecodeParams& p, const uint32_t* meta,
+                                               const uint8_t* blk, uint8_t* kbase, uint8_t* vbase,
+                                               uint32_t n, uint64_t en, uint64_t ek, uint64_t ev,
+                                               uint32_t off, uint32_t sub, uint32_t split,
+                                               bool mat, bool view, uint32_t lane) {
+  uint32_t carry = 0;  // key bytes of the entries before this chunk
+  for (uint32_t e0 = 0; e0 < n; e0 += kWave) {
+    const uint32_t e = e0 + lane;
+    const bool on = e < n;
+    const uint32_t m0 = meta[min(e, n)], m1 = meta[min(e + 1, n)];
+    const uint32_t hp = m0 & 0xffffu, vo = m0 >> 16;
+    const uint32_t vl = (m1 >> 16) - vo, kl = (m1 & 0xffffu) - hp - 10 - vl;
+    const uint32_t plen = on ? ((uint32_t)blk[hp] << 8) | blk[hp + 1] : 0u;
+    const uint32_t kout = on ? plen + kl : 0u;
+    const uint32_t incl = wave_scan_sat(kout, lane);
+    const uint32_t ko = carry + incl - kout;
+    carry += __builtin_amdgcn_readlane(incl, 63);
+    if (!on || (e / kWave) % split != sub) continue;
+    if (mat) {
+      if (p.key_end) p.key_end[en + e] = (uint32_t)(ek + ko + kout);
+      if (p.val_end) p.val_end[en + e] = (uint32_t)(ev + vo + vl);
+      if (kbase)
+        for (uint32_t i = 0; i < kout; i++)
+          kbase[ko + i] = i < plen ? blk[10 + i] : blk[hp + 10 + i - plen];
+      if (vbase)
+        for (uint32_t q = 0; q < pieces16(vl); q++) copy_piece16(vbase + vo, blk + hp + 10 + kl, vl, q);
     }
+    if (view)
+      p.view[en + e] = (uint64_t)(off + hp + 10) | ((uint64_t)kl << 32) | ((uint64_t)vl << 48);
   }
 }
 
@@ -548,10 +518,10 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   const uint32_t sub = wave % split;
   const uint32_t b = uniform(blockIdx.x * (4 / split) + wave / split);
   if (b >= p.nblk) return;
-  const uint2* meta = reinterpret_cast<const uint2*>(p.wmeta) + (uint64_t)b * p.wcap;
+  const uint32_t* meta = p.wmeta + (uint64_t)b * p.wcap;
   // the first 64 metadata records, one per lane, requested beside the per-block loads below
   // (one round trip fewer before the piece loads; records past the sentinel are never used)
-  const uint2 pre = meta[min(lane, p.wcap - 1)];
+  const uint32_t pre = meta[min(lane, p.wcap - 1)];
   const uint64_t* t = p.wstat + 3ull * b;
   const uint32_t n = uniform((uint32_t)t[0]), K = uniform((uint32_t)t[1]),
                  V = uniform((uint32_t)t[2]);
@@ -594,6 +564,13 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   // 119-B entries, 16 above 128 B (C5 Zipf keys: 0.96 vs 1.10 ms); p.wj forces 8 or 16.
   // 8 lanes x 5 groups = 40 entries per trip: every C2 block (31-37 entries) in one trip
   // (same-box A/B vs 4 groups: 0.799 -> 0.781 ms)
+  // a block with prefix-compressed entries: its K differs from the stored key bytes, which
+  // are the sentinel's position - 10 n - V
+  const uint32_t stop = uniform(meta[n] & 0xffffu);
+  if (K != stop - 10 * n - V) {
+    copy_entries_plen(p, meta, blk, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane);
+    return;
+  }
   const uint32_t avg = (K + V) / n;
   if (p.wj == 16 || (p.wj == 0 && avg > 128))
     copy_entries<16, 2>(p, meta, blk, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
