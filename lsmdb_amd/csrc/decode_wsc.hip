@@ -206,9 +206,15 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
           }
         }
       }
+      // the last chunk (the sentinel last) as whole 16-B parts of its 128-B line, by the group's
+      // L lanes (the general loop ran in lane 0: its count is the group's)
+      if (k == 0) row[gn & 31] = pos | (gV << 16);  // sentinel
+      const uint32_t gnl = (uint32_t)__shfl((int)gn, (int)gb);
+      wave_lds_fence();
+      for (uint32_t i = k; i < 8; i += L)
+        reinterpret_cast<uint4*>(meta + (gnl & ~31u))[i] =
+            make_uint4(row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3]);
       if (k == 0) {
-        row[gn & 31] = pos | (gV << 16);  // sentinel
-        flush_meta(meta + (gn & ~31u), row, (gn & 31) + 1);
         s_res[0][g] = gn;
         s_res[1][g] = gK;
         s_res[2][g] = gV;
@@ -288,10 +294,23 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
         }
       }
     }
+    // the last chunk (records n & ~31 .. n, the sentinel last) of every block, cooperatively as
+    // well: whole 128-B lines (the slot holds wcap records, a multiple of 32; words past the
+    // sentinel are never read)
+    if (valid) row[n & 31] = pos | (V << 16);
+    const uint64_t vm = __ballot(valid);
+    wave_lds_fence();
+#pragma unroll
+    for (uint32_t r = 0; r < 8; r++) {
+      const uint32_t L = 8 * r + (lane >> 3), part = lane & 7;
+      const uint32_t nL = (uint32_t)__shfl((int)n, (int)L);
+      if ((vm >> L) & 1ull) {
+        const uint32_t* rw = stage + (wave * 64 + L) * kWalkStage + 4 * part;
+        uint32_t* mL = p.wmeta + (uint64_t)(wb0 + L) * p.wcap + (nL & ~31u);
+        reinterpret_cast<uint4*>(mL)[part] = make_uint4(rw[0], rw[1], rw[2], rw[3]);
+      }
+    }
     if (valid) {
-      uint32_t* meta = p.wmeta + (uint64_t)b * p.wcap;
-      row[n & 31] = pos | (V << 16);
-      flush_meta(meta + (n & ~31u), row, (n & 31) + 1);
       uint64_t* t = p.wstat + 3ull * b;
       t[0] = n;
       t[1] = K;
