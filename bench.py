@@ -32,6 +32,7 @@ import json
 import os
 import socket
 import subprocess
+import tempfile
 import sys
 import time
 
@@ -63,10 +64,29 @@ def spawn_ranks(n: int, argv: list[str], timeout_s: float = 1800.0) -> int:
     stopped (they would wait at a barrier forever).  Returns the worst exit code."""
     port = _free_port()
     procs = []
+    # rank 0's stdout goes to a file and only its JSON line is forwarded to ours: the process
+    # group libraries print connection notices on stdout (gloo does), and the driver reads ONE
+    # JSON line.  Every other rank's stdout joins stderr.
+    out0 = tempfile.TemporaryFile(mode="w+")
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=out0 if r == 0 else sys.stderr))
+    try:
+        return _wait_ranks(procs, timeout_s)
+    finally:
+        out0.seek(0)
+        for line in out0:
+            if line.lstrip().startswith("{"):
+                sys.stdout.write(line)
+            else:
+                sys.stderr.write(line)
+        sys.stdout.flush()
+        out0.close()
+
+
+def _wait_ranks(procs: list, timeout_s: float) -> int:
     t0, rc = time.time(), 0
     live = list(procs)
     while live:

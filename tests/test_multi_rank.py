@@ -91,6 +91,7 @@ def test_bench_spawns_ranks_itself():
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1                          # rank 0 prints ONE line
+    assert out.stdout.strip() == lines[0]           # and nothing else: gloo's notices go to stderr
     j = json.loads(lines[0])
     assert j["n_gpus"] == 2 and j["total_bytes"] == 2 << 30 and len(j["per_rank_ms"]) == 2
     assert j["parity"] == "ok" and j["metric"].startswith("launcher self-test")
