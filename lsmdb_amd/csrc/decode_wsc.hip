@@ -63,7 +63,10 @@ __device__ __forceinline__ void read_hdr_nt(const uint8_t* g, uint32_t& plen, ui
 // records).  The walk stages 32 records per block in LDS and writes each chunk as one full
 // 128-B line -- 8-B stores straight from 64 lanes at 64 different blocks were evicted from L2 as
 // partial lines (4x the bytes).  Round 3: 4-B records instead of {pos | V << 16, K} (8 B).
-constexpr uint32_t kWalkStage = 33;  // u32 per lane row: 32 records + 1 pad (bank spread)
+constexpr uint32_t kWalkStage = 33;
+// p.wstatus[b] = the block's status | kPlenFlag when it holds prefix-compressed entries (the
+// walk's K exceeds the stored key bytes, stop pos - 10 n - V): the copy's header-reading path
+constexpr uint32_t kPlenFlag = 1u << 16;  // u32 per lane row: 32 records + 1 pad (bank spread)
 
 __device__ __forceinline__ void flush_meta(uint32_t* dst, const uint32_t* row, uint32_t cnt) {
   if (cnt == 32) {
@@ -218,7 +221,8 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
         s_res[0][g] = gn;
         s_res[1][g] = gK;
         s_res[2][g] = gV;
-        s_res[3][g] = gst;
+        // + kPlenFlag: the block holds prefix-compressed entries (K exceeds the stored key bytes)
+        s_res[3][g] = gst | (gK != pos - 10 * gn - gV ? kPlenFlag : 0u);
         s_off[g] = off;
       }
     }
@@ -227,12 +231,13 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
       n = s_res[0][tid];
       K = s_res[1][tid];
       V = s_res[2][tid];
-      st = s_res[3][tid];
+      const uint32_t sw = s_res[3][tid];
+      st = sw & ~kPlenFlag;
       uint64_t* t = p.wstat + 3ull * b;
       t[0] = n;
       t[1] = K;
       t[2] = V;
-      p.wstatus[b] = st;
+      p.wstatus[b] = sw;
     }
   } else {
     // Lane walk, records flushed cooperatively: every lane walks in lockstep (a lane that
@@ -315,7 +320,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
       t[0] = n;
       t[1] = K;
       t[2] = V;
-      p.wstatus[b] = st;
+      p.wstatus[b] = st | (K != pos - 10 * n - V ? kPlenFlag : 0u);  // see kPlenFlag
     }
   }
   // tile scan (saturating u32: a key stream past 4 GiB - 1 fails the copy's capacity check)
@@ -568,7 +573,7 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   const uint64_t* t = p.wstat + 3ull * b;
   const uint32_t n = uniform((uint32_t)t[0]), K = uniform((uint32_t)t[1]),
                  V = uniform((uint32_t)t[2]);
-  const uint32_t st = uniform(p.wstatus[b]);
+  const uint32_t sw = uniform(p.wstatus[b]), st = sw & ~kPlenFlag;
   const uint64_t* bs = p.wbase + 3ull * b;
   const uint64_t en = uniform64(bs[0]), ek = uniform64(bs[1]), ev = uniform64(bs[2]);
   const uint32_t off = uniform(p.blk_off[b]);
@@ -607,10 +612,8 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   // 119-B entries, 16 above 128 B (C5 Zipf keys: 0.96 vs 1.10 ms); p.wj forces 8 or 16.
   // 8 lanes x 5 groups = 40 entries per trip: every C2 block (31-37 entries) in one trip
   // (same-box A/B vs 4 groups: 0.799 -> 0.781 ms)
-  // a block with prefix-compressed entries: its K differs from the stored key bytes, which
-  // are the sentinel's position - 10 n - V
-  const uint32_t stop = uniform(meta[n] & 0xffffu);
-  if (K != stop - 10 * n - V) {
+  // a block with prefix-compressed entries (flagged by the walk: no load of the sentinel here)
+  if (sw & kPlenFlag) {
     copy_entries_plen(p, meta, blk, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane);
     return;
   }
