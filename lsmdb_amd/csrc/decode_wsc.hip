@@ -411,24 +411,42 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     for (uint32_t i = 0; i < n; i++) owner[f + i] = (Owner)tid;
     __syncthreads();
   }
-  for (uint32_t e = tid; e < nt; e += 256) {
-    uint32_t lo = 0, hi = 255;
-    if (mapped) {
-      lo = owner[e];
-    } else {
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1) >> 1;
-        if (s_first[mid] <= e) lo = mid; else hi = mid - 1;
+  // 4 entries per thread per trip, every record load issued before any view store (the
+  // compiler keeps a load behind an earlier store it cannot prove apart)
+  constexpr uint32_t kVB = 4;
+  for (uint32_t eb = tid; eb < nt; eb += 256 * kVB) {
+    uint32_t m0[kVB], m1[kVB], lo[kVB];
+    bool on[kVB];
+#pragma unroll
+    for (uint32_t u = 0; u < kVB; u++) {
+      const uint32_t e = eb + 256 * u;
+      uint32_t l = 0, hi = 255;
+      if (e < nt) {
+        if (mapped) {
+          l = owner[e];
+        } else {
+          while (l < hi) {
+            const uint32_t mid = (l + hi + 1) >> 1;
+            if (s_first[mid] <= e) l = mid; else hi = mid - 1;
+          }
+        }
       }
+      lo[u] = l;
+      const uint64_t bend = e0 + s_first[l + 1];
+      on[u] = e < nt && bend <= p.ent_cap && bend <= 0xffffffffull;  // else reported (result[5])
+      const uint32_t i = on[u] ? e - s_first[l] : 0u;
+      const uint32_t* meta = p.wmeta + (uint64_t)(tile * TB + l) * p.wcap;
+      m0[u] = meta[i];
+      m1[u] = meta[i + 1];
     }
-    const uint64_t bend = e0 + s_first[lo + 1];
-    if (bend > p.ent_cap || bend > 0xffffffffull) continue;  // reported above (result[5])
-    const uint32_t i = e - s_first[lo];
-    const uint32_t* meta = p.wmeta + (uint64_t)(tile * TB + lo) * p.wcap;
-    const uint32_t m0 = meta[i], m1 = meta[i + 1];
-    const uint32_t hp = m0 & 0xffffu, vl = (m1 >> 16) - (m0 >> 16);
-    const uint32_t kl = (m1 & 0xffffu) - hp - 10 - vl;  // stored key bytes
-    p.view[e0 + e] = (uint64_t)(s_off[lo] + hp + 10) | ((uint64_t)kl << 32) | ((uint64_t)vl << 48);
+#pragma unroll
+    for (uint32_t u = 0; u < kVB; u++) {
+      if (!on[u]) continue;
+      const uint32_t hp = m0[u] & 0xffffu, vl = (m1[u] >> 16) - (m0[u] >> 16);
+      const uint32_t kl = (m1[u] & 0xffffu) - hp - 10 - vl;  // stored key bytes
+      p.view[e0 + eb + 256 * u] =
+          (uint64_t)(s_off[lo[u]] + hp + 10) | ((uint64_t)kl << 32) | ((uint64_t)vl << 48);
+    }
   }
 }
 
