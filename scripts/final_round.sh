@@ -7,4 +7,4 @@ timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -1 gpurun_out/final_tests.log
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/final_smoke.log 2>&1 || { tail -20 gpurun_out/final_smoke.log; exit 1; }
 tail -1 gpurun_out/final_smoke.log
-bash scripts/profile_round.sh r03p && python -c "import json;j=json.load(open('gpurun_out/prof_r03p/bench.json'));k=j['roofline']['kernels'];print('bench',j['value'],j['ms_per_step'],k['walk_ms'],k['copy_ms'],'view',j['view_mode']['gibs_per_gpu'])"
+bash scripts/profile_round.sh r03r && python -c "import json;j=json.load(open('gpurun_out/prof_r03r/bench.json'));k=j['roofline']['kernels'];print('bench',j['value'],j['ms_per_step'],k['walk_ms'],k['copy_ms'],'view',j['view_mode']['gibs_per_gpu'])"
