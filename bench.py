@@ -134,9 +134,12 @@ def build_device_sst(codec, torch, dev, cfg: int, target_bytes: int, shard: int)
         kt, vt = int(cols.key_end[n - 1]), int(cols.vs_end[n - 1])
         cols = workload.Columns(cols.keys[:kt], cols.key_end[:n], cols.vs[:vt], cols.vs_end[:n],
                                 cols.entries_per_block, cols.block_bytes)
-    else:
+    else:  # at least target_bytes of block data: generated long, trimmed at the exact size
         n = workload.entries_for_bytes(cfg, target_bytes)
         cols = workload.config_columns(cfg, n, seed_offset=shard)
+        plan = C.plan_blocks(cols.key_end, cols.vs_end, cols.entries_per_block, cols.block_bytes)
+        cols = workload.trim_to_bytes(cols, plan, target_bytes)
+        n = cols.n
     plan = C.plan_blocks(cols.key_end, cols.vs_end, cols.entries_per_block, cols.block_bytes)
     nblocks = plan.size - 1
     key_total, vs_total = int(cols.key_end[-1]), int(cols.vs_end[-1])
@@ -247,7 +250,31 @@ def time_decode(codec, torch, w, bufs, mode: int, steps: int, warmup: int, dist=
     return wall, float(np.mean(kms)), float(np.median(kms))
 
 
-def kernel_split(codec, w, bufs, mode: int, reps: int = 10):
+def walk_fetch_bytes(torch, w, view, blk_first) -> int:
+    """The bytes the walk must fetch from HBM: every 128-B line holding one of the 8-B header
+    reads it makes -- each entry's header and each block's stop header (the terminator, or the
+    header it stops at), iterator.go:112-135.  Computed from a view decode's records (key
+    position, klen, vlen per entry) and the block list, on the device.  For C2's 129-B entries
+    this is every line of the input; for C3's 1,101-B entries about 4 lines of a block's 26."""
+    n = int(blk_first[-1].item())
+    v = view[:n].to(torch.int64)
+    kp = v & 0xFFFFFFFF
+    kl = (v >> 32) & 0xFFFF
+    vl = (v >> 48) & 0xFFFF
+    heads = [kp - 10]
+    bf = blk_first.to(torch.int64)
+    cnt = bf[1:] - bf[:-1]
+    off = w["d_off"].to(torch.int64) & 0xFFFFFFFF
+    ln = w["d_len"].to(torch.int64) & 0xFFFFFFFF
+    last = torch.clamp(bf[1:] - 1, min=0)
+    stop = torch.where(cnt > 0, kp[last] + kl[last] + vl[last] if n else off, off)
+    heads.append(stop[stop + 10 <= off + ln])  # a header read only where 10 bytes remain
+    h = torch.cat(heads)
+    lines = torch.unique(torch.cat([h >> 7, (h + 7) >> 7]))
+    return int(lines.numel()) * 128
+
+
+def kernel_split(codec, w, bufs, mode: int, reps: int = 10, fetch: int = 0):
     """Walk and copy durations of the walk-scan-copy decode, from HIP events the library records
     on its stream between its two launches (lsmgpu_kernel_times), outside the timed loop.  The
     copy's bytes: key + vs bytes read and written, u32 key_end + val_end per entry, blk_first +
@@ -272,10 +299,15 @@ def kernel_split(codec, w, bufs, mode: int, reps: int = 10):
         codec.set_kernel_timing(False)
     wm, cm = float(np.mean(walk)), float(np.mean(copy))
     copy_bytes = 2 * (w["key_total"] + w["vs_total"]) + 8 * w["n"] + 8 * w["nblocks"]
+    walk_bytes = fetch + 8 * w["nblocks"]  # header lines + (off, len) per block
     return {"walk_ms": round(wm, 4), "copy_ms": round(cm, 4),
+            # the input rate (bytes of blocks walked / time): NOT a roofline fraction
             "walk_input_gbs": round(w["data_len"] / (wm / 1e3) / 1e9, 1),
-            "walk_read_frac": round(w["data_len"] / (wm / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            # roofline: the lines the walk must fetch (walk_fetch_bytes) / time / peak
+            "walk_fetch_bytes": walk_bytes,
+            "walk_read_frac": round(walk_bytes / (wm / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             "copy_gbs": round(copy_bytes / (cm / 1e3) / 1e9, 1) if cm > 0 else None,
+            "copy_frac": round(copy_bytes / (cm / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if cm > 0 else None,
             "copy_algorithmic_bytes": copy_bytes,
             "source": "HIP events recorded by the library around its walk and copy launches"}
 
@@ -291,7 +323,9 @@ def practical_peaks(codec, torch, dev, nbytes: int, reps: int = 7) -> dict:
     dst = torch.empty_like(src)
     stream = torch.cuda.current_stream()
     best = {}
-    for kind, name, mult in ((0, "copy", 2), (2, "copy_nt", 2), (1, "read", 1), (3, "read_nt", 1)):
+    kinds = ((0, "copy", 2), (2, "copy_nt", 2), (4, "copy_u16", 2), (6, "copy_nt_u16", 2),
+             (1, "read", 1), (3, "read_nt", 1), (5, "read_u16", 1), (7, "read_nt_u16", 1))
+    for kind, name, mult in kinds:
         for wg in (2, 4, 8, 16):
             codec.stream_probe_async(kind, src, dst, nbytes, wg)
             ts = []
@@ -303,14 +337,15 @@ def practical_peaks(codec, torch, dev, nbytes: int, reps: int = 7) -> dict:
                 b.synchronize()
                 ts.append(a.elapsed_time(b))
             gbs = mult * nbytes / (float(np.median(ts)) / 1e3) / 1e9
-            fam = "copy" if kind in (0, 2) else "read"
+            fam = "read" if kind & 1 else "copy"
             if gbs > best.get(fam, (0,))[0]:
                 best[fam] = (gbs, f"{name}, {wg} workgroups/CU")
     del src, dst
     return {"copy_gbs": round(best["copy"][0], 1), "copy_kind": best["copy"][1],
             "read_gbs": round(best["read"][0], 1), "read_kind": best["read"][1],
             "bytes": nbytes, "source": "lsmgpu_stream_probe_async (csrc/probe.hip), best of "
-                                       "default / nt policies at 2-16 workgroups per CU"}
+                                       "default / nt policies, 4 or 16 16-B loads in flight per "
+                                       "lane, 2-16 workgroups per CU"}
 
 
 def check_round_trip(torch, w, bufs) -> str:
@@ -483,24 +518,35 @@ def run_rank(args) -> None:
     bufs = codec.alloc_decode(w["data_len"], w["data_len"], w["nblocks"], mode, ent_cap=w["n"])
     wall, kms_mean, kms_med = time_decode(codec, torch, w, bufs, mode, args.steps, args.warmup, dist)
     parity = check_round_trip(torch, w, bufs)
-    split = kernel_split(codec, w, bufs, mode)
+
+    # the lines the walk must fetch, from one view decode's records (outside any timed region)
+    vbufs = codec.alloc_decode(w["data_len"], 0, w["nblocks"], MODE_VIEW, ent_cap=w["n"])
+    codec.decode_device_async(w["d_sst"], w["d_off"], w["d_len"], w["max_len"], MODE_VIEW, vbufs,
+                              data_len=w["data_len"])
+    torch.cuda.synchronize()
+    fetch = walk_fetch_bytes(torch, w, vbufs.view, vbufs.blk_first)
+    split = kernel_split(codec, w, bufs, mode, fetch=fetch)
 
     view = None
     if not args.no_view:
-        vbufs = codec.alloc_decode(w["data_len"], 0, w["nblocks"], MODE_VIEW, ent_cap=w["n"])
         vwall, vk, _ = time_decode(codec, torch, w, vbufs, MODE_VIEW, args.steps, args.warmup, dist)
-        vr, vw = algorithmic_bytes(w, MODE_VIEW)
+        _, vw = algorithmic_bytes(w, MODE_VIEW)
+        vread = fetch + 8 * w["nblocks"]  # the header lines + (off, len) per block
         view = {"gibs_per_gpu": round(w["data_len"] / (vk / 1e3) / (1 << 30), 2),
-                "kernel_ms": round(vk, 4), "achieved_gbs": round((vr + vw) / (vk / 1e3) / 1e9, 1),
-                "frac": round((vr + vw) / (vk / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                # the north star's metric: input bytes / kernel time against the HBM-read peak
-                "read_frac": round(w["data_len"] / (vk / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
-        del vbufs
+                "kernel_ms": round(vk, 4),
+                "achieved_gbs": round((vread + vw) / (vk / 1e3) / 1e9, 1),
+                "frac": round((vread + vw) / (vk / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                # the north star's HBM-read roofline: the bytes view mode must fetch (every
+                # 128-B line holding a header) / kernel time / 8 TB/s
+                "read_frac": round(fetch / (vk / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                "fetch_bytes": fetch,
+                "input_gbs": round(w["data_len"] / (vk / 1e3) / 1e9, 1)}
+    del vbufs
 
     practical = None if args.no_peaks else practical_peaks(codec, torch, dev, w["data_len"])
     if view is not None and practical is not None:
         view["read_frac_of_practical"] = round(
-            w["data_len"] / (view["kernel_ms"] / 1e3) / 1e9 / practical["read_gbs"], 4)
+            fetch / (view["kernel_ms"] / 1e3) / 1e9 / practical["read_gbs"], 4)
     encode = time_encode(codec, torch, w, min(args.steps, 10))
 
     wall, parity, total_bytes, per_rank = reduce_over_ranks(dist, torch, coll_dev, wall, parity,

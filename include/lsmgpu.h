@@ -24,7 +24,9 @@
 extern "C" {
 #endif
 
-#define LSMGPU_ABI_VERSION 1
+/* 2 (round 4): size queries (decode with every output pointer NULL, encode with out == NULL),
+ * LSMGPU_ERR_CORRUPT, stream probe kinds 4-7 and its argument checks. */
+#define LSMGPU_ABI_VERSION 2
 
 /* ---- call status ---- */
 #define LSMGPU_OK 0
@@ -69,10 +71,11 @@ int lsmgpu_synchronize(lsmgpu_ctx* ctx);
 int lsmgpu_set_kernel_timing(lsmgpu_ctx* ctx, int on);
 int lsmgpu_kernel_times(lsmgpu_ctx* ctx, float* walk_ms, float* copy_ms);
 /* Diagnostics (no reference counterpart): the practical HBM ceilings bench.py prices the decode
- * against -- a grid-stride 16-B-per-lane streaming copy (kind 0; 2 = non-temporal loads and
- * stores) or read (kind 1; 3 = non-temporal) of `bytes` (a multiple of 16) from d_src (to d_dst;
- * for a read, d_dst is a 4-B sink), wg_per_cu 256-thread workgroups per CU.  Asynchronous on
- * the ctx stream. */
+ * against -- a grid-stride 16-B-per-lane streaming copy or read of `bytes` from d_src (to d_dst;
+ * for a read, d_dst is a 4-B sink), wg_per_cu 256-thread workgroups per CU.  kind bit 0: read
+ * (else copy); bit 1: non-temporal loads and stores; bit 2: 16 loads in flight per lane (else 4).
+ * `bytes` must be a multiple of 16 and both pointers 16-B aligned (else LSMGPU_ERR_ARG).
+ * Asynchronous on the ctx stream. */
 int lsmgpu_stream_probe_async(lsmgpu_ctx* ctx, int kind, const void* d_src, void* d_dst,
                               uint64_t bytes, uint32_t wg_per_cu);
 const char* lsmgpu_strerror(int code);

@@ -8,7 +8,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "lsmdb_amd", "csrc")
 LIB = os.path.join(ROOT, "lsmdb_amd", "liblsmgpu.so")
-SOURCES = ["api.hip", "decode.hip", "decode_wsc.hip", "encode.hip", "open_tables.hip", "merge.hip", "bloom.hip", "probe.hip"]
+SOURCES = ["api.hip", "decode.hip", "decode_wsc.hip", "decode_onepass.hip", "encode.hip", "open_tables.hip", "merge.hip", "bloom.hip", "probe.hip"]
 HEADERS = ["codec_common.hpp", "decode_common.hpp", "kernels.hpp", os.path.join("..", "..", "include", "lsmgpu.h")]
 ARCH = os.environ.get("LSMGPU_ARCH", "gfx950")
 
@@ -21,14 +21,28 @@ def _stale(target: str, deps: list[str]) -> bool:
 
 
 def build_lib(force: bool = False, verbose: bool = True) -> str:
+    """Each source compiled to its own object in parallel (build/), then one link."""
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
     if not force and not _stale(LIB, deps):
         return LIB
-    cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-o", LIB] + [os.path.join(CSRC, s) for s in SOURCES]
+    flags = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall"]
+    lib = LIB
     if os.environ.get("LSMGPU_BUILD_STAMPS"):  # diagnostic build: per-phase s_memtime stamps
-        cmd.insert(1, "-DLSMGPU_STAMPS")
-        cmd[cmd.index(LIB)] = LIB.replace("liblsmgpu.so", "liblsmgpu_stamps.so")
+        flags.append("-DLSMGPU_STAMPS")
+        lib = LIB.replace("liblsmgpu.so", "liblsmgpu_stamps.so")
+    objdir = os.path.join(ROOT, "lsmdb_amd", "build")
+    os.makedirs(objdir, exist_ok=True)
+    jobs, objs = [], []
+    for s in SOURCES:
+        obj = os.path.join(objdir, os.path.splitext(s)[0] + ".o")
+        objs.append(obj)
+        cmd = flags + ["-c", "-o", obj, os.path.join(CSRC, s)]
+        if verbose:
+            print("[build]", " ".join(cmd), file=sys.stderr)
+        jobs.append(subprocess.Popen(cmd, cwd=CSRC))
+    if any(j.wait() != 0 for j in jobs):
+        raise subprocess.CalledProcessError(1, "hipcc")
+    cmd = flags + ["-shared", "-o", lib] + objs
     if verbose:
         print("[build]", " ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=CSRC)

@@ -188,8 +188,10 @@ int lsmgpu_kernel_times(lsmgpu_ctx* c, float* walk_ms, float* copy_ms) {
 
 int lsmgpu_stream_probe_async(lsmgpu_ctx* c, int kind, const void* d_src, void* d_dst,
                               uint64_t bytes, uint32_t wg_per_cu) {
-  if (!c || !d_src || !d_dst || kind < 0 || kind > 3 || wg_per_cu == 0 || wg_per_cu > 64)
+  if (!c || !d_src || !d_dst || kind < 0 || kind > 7 || wg_per_cu == 0 || wg_per_cu > 64)
     return LSMGPU_ERR_ARG;
+  // uint4 loads / stores: whole 16-B words at 16-B aligned addresses only
+  if (bytes % 16 != 0 || ((uintptr_t)d_src | (uintptr_t)d_dst) % 16 != 0) return LSMGPU_ERR_ARG;
   HIPC(hipSetDevice(c->device));
   HIPC(launch_stream_probe(kind, d_src, d_dst, bytes, wg_per_cu * (uint32_t)c->num_cus, c->stream));
   return LSMGPU_OK;
@@ -333,6 +335,21 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
       const int l = atoi(wk_env + 5);  // "group" alone: 8 lanes
       p.wwalk = kWalkGroup;
       p.wlanes = l == 2 || l == 4 || l == 16 ? (uint32_t)l : 8u;  // "group2" ... "group16"
+    }
+    // one-pass decode (decode_onepass.hip): LSMGPU_DECODE_PATH=one
+    const char* dp_env = getenv("LSMGPU_DECODE_PATH");
+    const bool onepass_env = dp_env && strncmp(dp_env, "one", 3) == 0;
+    if (onepass_env) {
+      HIPC(hipMemsetAsync(d_result, 0, 8 * sizeof(uint64_t), c->stream));
+      if (c->ktime) HIPC(hipEventRecord(c->kev[0], c->stream));
+      HIPC(launch_decode_onepass(p, max_blk_len, c->num_cus, c->stream));
+      if (c->ktime) {
+        HIPC(hipEventRecord(c->kev[1], c->stream));
+        HIPC(hipEventRecord(c->kev[2], c->stream));
+      }
+      c->kvalid = c->ktime;
+      c->kfused = true;
+      return LSMGPU_OK;
     }
     // d_result is zeroed by the walk kernel when a copy launch follows it (the copy's atomics
     // come after the kernel boundary): one operation fewer per decode.  A view-only decode
@@ -1134,7 +1151,7 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
     base[t + 1] = base[t] + dend;
     tblk[t + 1] = (uint32_t)off.size();
   }
-  const uint64_t nblk = off.size(), data_len = base[ntables];
+  const uint64_t data_len = base[ntables];
   if (data_len > 0xffffffffull) return LSMGPU_ERR_TOO_LARGE;
   // 2. inputs to HBM, one decode over every block of every input (materialize)
   HIPC(c->cp_data.ensure(data_len + 64));
@@ -1142,66 +1159,123 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
     if (base[t + 1] > base[t])
       HIPC(hipMemcpyAsync(c->cp_data.as<uint8_t>() + base[t], ssts[t], base[t + 1] - base[t],
                           hipMemcpyHostToDevice, c->stream));
-  HIPC(c->cp_off.ensure(nblk * 4 + 4));
-  HIPC(c->cp_len.ensure(nblk * 4 + 4));
-  if (nblk) {
-    HIPC(hipMemcpyAsync(c->cp_off.p, off.data(), nblk * 4, hipMemcpyHostToDevice, c->stream));
-    HIPC(hipMemcpyAsync(c->cp_len.p, len.data(), nblk * 4, hipMemcpyHostToDevice, c->stream));
-  }
   HIPC(c->cp_res.ensure(64));
   uint64_t* d_res = c->cp_res.as<uint64_t>();
-  uint64_t kcap = std::max<uint64_t>(data_len, 16), vcap = kcap, ecap = data_len / 10 + 1;
   uint64_t r[8];
-  for (int attempt = 0;; attempt++) {  // plen > 0 blocks can expand keys: resize once
-    HIPC(c->cp_kd.ensure(kcap + 16));
-    HIPC(c->cp_vd.ensure(vcap + 16));
-    HIPC(c->cp_ke.ensure(ecap * 4 + 4));
-    HIPC(c->cp_ve.ensure(ecap * 4 + 4));
-    HIPC(c->cp_bf.ensure(nblk * 4 + 4));
-    HIPC(c->cp_bs.ensure(nblk * 4 + 4));
-    lsmgpu_decoded d{};
-    d.key_data = c->cp_kd.as<uint8_t>();
-    d.key_cap = kcap;
-    d.key_end = c->cp_ke.as<uint32_t>();
-    d.val_data = c->cp_vd.as<uint8_t>();
-    d.val_cap = vcap;
-    d.val_end = c->cp_ve.as<uint32_t>();
-    d.ent_cap = ecap;
-    d.blk_first = c->cp_bf.as<uint32_t>();
-    d.blk_status = c->cp_bs.as<int32_t>();
-    int rc = lsmgpu_decode_blocks_async(c, c->cp_data.as<uint8_t>(), data_len,
-                                        c->cp_off.as<uint32_t>(), c->cp_len.as<uint32_t>(), nblk,
-                                        max_len, LSMGPU_MODE_MATERIALIZE, &d, d_res);
-    if (rc != LSMGPU_OK) return rc;
-    HIPC(hipMemcpyAsync(r, d_res, 64, hipMemcpyDeviceToHost, c->stream));
+  // one materialize decode of the block list (o, l); blk_first / blk_status come back to bf / bs
+  std::vector<uint32_t> bf, bs;
+  auto decode_list = [&](const std::vector<uint32_t>& o, const std::vector<uint32_t>& l) -> int {
+    const uint64_t nb = o.size();
+    HIPC(c->cp_off.ensure(nb * 4 + 4));
+    HIPC(c->cp_len.ensure(nb * 4 + 4));
+    if (nb) {
+      HIPC(hipMemcpyAsync(c->cp_off.p, o.data(), nb * 4, hipMemcpyHostToDevice, c->stream));
+      HIPC(hipMemcpyAsync(c->cp_len.p, l.data(), nb * 4, hipMemcpyHostToDevice, c->stream));
+    }
+    uint64_t kcap = std::max<uint64_t>(data_len, 16), vcap = kcap, ecap = data_len / 10 + 1;
+    for (int attempt = 0;; attempt++) {  // plen > 0 blocks can expand keys: resize once
+      HIPC(c->cp_kd.ensure(kcap + 16));
+      HIPC(c->cp_vd.ensure(vcap + 16));
+      HIPC(c->cp_ke.ensure(ecap * 4 + 4));
+      HIPC(c->cp_ve.ensure(ecap * 4 + 4));
+      HIPC(c->cp_bf.ensure(nb * 4 + 4));
+      HIPC(c->cp_bs.ensure(nb * 4 + 4));
+      lsmgpu_decoded d{};
+      d.key_data = c->cp_kd.as<uint8_t>();
+      d.key_cap = kcap;
+      d.key_end = c->cp_ke.as<uint32_t>();
+      d.val_data = c->cp_vd.as<uint8_t>();
+      d.val_cap = vcap;
+      d.val_end = c->cp_ve.as<uint32_t>();
+      d.ent_cap = ecap;
+      d.blk_first = c->cp_bf.as<uint32_t>();
+      d.blk_status = c->cp_bs.as<int32_t>();
+      int rc = lsmgpu_decode_blocks_async(c, c->cp_data.as<uint8_t>(), data_len,
+                                          c->cp_off.as<uint32_t>(), c->cp_len.as<uint32_t>(), nb,
+                                          max_len, LSMGPU_MODE_MATERIALIZE, &d, d_res);
+      if (rc != LSMGPU_OK) return rc;
+      HIPC(hipMemcpyAsync(r, d_res, 64, hipMemcpyDeviceToHost, c->stream));
+      HIPC(hipStreamSynchronize(c->stream));
+      if (r[5] & 2) return LSMGPU_ERR_INTERNAL;
+      if (!(r[5] & 1)) break;
+      if (attempt) return LSMGPU_ERR_CAPACITY;
+      kcap = std::max<uint64_t>(r[1], 16);
+      vcap = std::max<uint64_t>(r[2], 16);
+      ecap = std::max<uint64_t>(r[0], 1);
+    }
+    bf.assign(nb + 1, 0);
+    bs.assign(nb + 1, 0);
+    HIPC(hipMemcpyAsync(bf.data(), c->cp_bf.p, (nb + 1) * 4, hipMemcpyDeviceToHost, c->stream));
+    if (nb) HIPC(hipMemcpyAsync(bs.data(), c->cp_bs.p, nb * 4, hipMemcpyDeviceToHost, c->stream));
     HIPC(hipStreamSynchronize(c->stream));
-    if (r[5] & 2) return LSMGPU_ERR_INTERNAL;
-    if (!(r[5] & 1)) break;
-    if (attempt) return LSMGPU_ERR_CAPACITY;
-    kcap = std::max<uint64_t>(r[1], 16);
-    vcap = std::max<uint64_t>(r[2], 16);
-    ecap = std::max<uint64_t>(r[0], 1);
+    return LSMGPU_OK;
+  };
+  int drc = decode_list(off, len);
+  if (drc != LSMGPU_OK) return drc;
+  // Which decoded entries Go's iterators reach (levels.go:243-253, table/iterator.go:183,
+  // 201-217,301-326,412-496, y/iterator.go:128-147): tables were opened by OpenTable first.
+  const int32_t kOk = LSMGPU_BLK_OK, kVo = LSMGPU_BLK_VALUE_OVERFLOW;
+  std::vector<uint8_t> rewind_ok(ntables, 0), visited(ntables, 0);
+  for (uint32_t t = 0; t < ntables; t++) {
+    const uint32_t b0 = tblk[t], b1 = tblk[t + 1];
+    for (uint32_t b = b0; b < b1; b++) {
+      const uint32_t nb = bf[b + 1] - bf[b];
+      const int32_t st = bs[b];
+      // readIndex asserts plen == 0 on every block's first header (table.go:239): log.Fatal
+      if (nb == 0 && st == LSMGPU_BLK_FIRST_PLEN) return LSMGPU_ERR_CORRUPT;
+      // a terminator-first block of a multi-block table: readIndex's sort compares its empty
+      // first key (table.go:267 -> y.CompareKeys' len > 8 assertion, y.go:85)
+      if (nb == 0 && st == kOk && len[b] >= 10 && b1 - b0 >= 2) return LSMGPU_ERR_CORRUPT;
+      // NewIterator runs block 0's first Next (iterator.go:183): a truncated first header panics
+      if (b == b0 && nb == 0 && st == LSMGPU_BLK_TRUNC_HEADER) return LSMGPU_ERR_CORRUPT;
+    }
+    // Rewind = seekToFirst: valid only when block 0 yields an entry (iterator.go:201-217)
+    rewind_ok[t] = b1 > b0 && bf[b0 + 1] > bf[b0];
   }
-  // A value overflow ends Go's block iterator after the entries before it, and Iterator.next
-  // moves on to the next block (iterator.go:103-106,318-323): the decoded stream already holds
-  // exactly those entries.  Every other status is a Go panic / log.Fatal: corrupt input.
-  if (r[4]) {
-    std::vector<int32_t> bs(nblk);
-    HIPC(hipMemcpyAsync(bs.data(), c->cp_bs.p, nblk * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPC(hipStreamSynchronize(c->stream));
-    for (int32_t s : bs)
-      if (s != LSMGPU_BLK_OK && s != LSMGPU_BLK_VALUE_OVERFLOW) return LSMGPU_ERR_CORRUPT;
+  // every run is a ConcatIterator (a single table behaves the same): its Rewind rewinds only the
+  // first table -- if that one is invalid the MergeIterator drops the whole run (initHeap);
+  // otherwise Next skips the later tables whose Rewind is invalid
+  for (uint32_t k = 0; k < nruns; k++) {
+    const uint32_t a = run_first[k], e = run_first[k + 1];
+    if (a == e || !rewind_ok[a]) continue;
+    for (uint32_t t = a; t < e; t++) visited[t] = rewind_ok[t];
+  }
+  bool filter = false;
+  for (uint32_t t = 0; t < ntables; t++) {
+    const uint32_t b0 = tblk[t], b1 = tblk[t + 1];
+    if (!visited[t]) {
+      filter = filter || bf[b1] > bf[b0];  // entries Go never reaches
+      continue;
+    }
+    for (uint32_t b = b0; b < b1; b++) {
+      // Iterator.next into a block that yields nothing returns Valid with a nil key: the merge
+      // then compares it (y.CompareKeys asserts) or Value() panics in Decode (iterator.go:312-313)
+      if (b != b0 && bf[b + 1] == bf[b]) return LSMGPU_ERR_CORRUPT;
+      // a truncated header or a prefix past the base key panics when the iterator reaches it; a
+      // value overflow ends the block after the entries before it (iterator.go:103-106,318-323)
+      if (bs[b] != kOk && bs[b] != kVo) return LSMGPU_ERR_CORRUPT;
+    }
+  }
+  if (filter) {  // rare (corrupt input): decode again without the tables Go never reaches
+    std::vector<uint32_t> o2, l2;
+    std::vector<uint32_t> tb2(ntables + 1, 0);
+    for (uint32_t t = 0; t < ntables; t++) {
+      if (visited[t])
+        for (uint32_t b = tblk[t]; b < tblk[t + 1]; b++) {
+          o2.push_back(off[b]);
+          l2.push_back(len[b]);
+        }
+      tb2[t + 1] = (uint32_t)o2.size();
+    }
+    tblk.swap(tb2);
+    drc = decode_list(o2, l2);
+    if (drc != LSMGPU_OK) return drc;
   }
   const uint64_t n = r[0];
   if (n > 0xfffffffeull) return LSMGPU_ERR_TOO_LARGE;
   // 3. runs in entries: run r = the entries of tables [run_first[r], run_first[r+1])
   std::vector<uint32_t> rf(nruns + 1);
-  {
-    std::vector<uint32_t> bf(nblk + 1);
-    HIPC(hipMemcpyAsync(bf.data(), c->cp_bf.p, (nblk + 1) * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPC(hipStreamSynchronize(c->stream));
-    for (uint32_t k = 0; k <= nruns; k++) rf[k] = bf[tblk[run_first[k]]];
-  }
+  for (uint32_t k = 0; k <= nruns; k++) rf[k] = bf[tblk[run_first[k]]];
   if (n == 0) {  // every input empty: the Go loop builds no table
     c->cp_tbl_out.assign(1, 0);
     c->cp_bytes = 0;

@@ -21,8 +21,10 @@
 // Blocks larger than the slot, with more entries than the metadata holds, or with prefix-
 // compressed keys (plen > 0: never written by table.Builder) take a global-memory
 // path with identical semantics.
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 
 #include "codec_common.hpp"
 #include "decode_common.hpp"
@@ -1167,8 +1169,13 @@ static int resident_per_cu(const DecodeParams& p, int num_cus, hipStream_t s) {
   using Cfg = T;
   auto k = T::kernel();
   const int SLOT = T::kSlot;
-  static int per_cu = 0;
-  if (per_cu) return per_cu;
+  static std::atomic<int> per_cu_cached{0};
+  if (int v = per_cu_cached.load(std::memory_order_acquire)) return v;
+  // one census per configuration and process, even with contexts on several threads
+  static std::mutex census_mu;
+  std::lock_guard<std::mutex> lock(census_mu);
+  if (int v = per_cu_cached.load(std::memory_order_acquire)) return v;
+  int per_cu = 0;
   if (Cfg::kLds > 64 * 1024 &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                           hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::kLds) != hipSuccess)
@@ -1200,6 +1207,7 @@ static int resident_per_cu(const DecodeParams& p, int num_cus, hipStream_t s) {
   }
   (void)hipFree(c);
   per_cu = found;
+  per_cu_cached.store(per_cu, std::memory_order_release);
   if (getenv("LSMGPU_DEBUG"))
     fprintf(stderr, "[lsmgpu] decode SLOT=%d census: api %d lds %d -> resident %d per CU\n", SLOT,
             api, Cfg::kLds, per_cu);
@@ -1261,9 +1269,9 @@ static hipError_t launch_cfg(const DecodeParams& p, int num_cus, hipStream_t s,
 }
 
 int decode_path(uint32_t max_blk_len, uint32_t nblk) {
-  // LSMGPU_DECODE_PATH=reg|lds|wsc forces a path (A/B diagnostics and tests)
+  // LSMGPU_DECODE_PATH=reg|lds|wsc|one forces a path (A/B diagnostics and tests)
   const char* f = getenv("LSMGPU_DECODE_PATH");
-  if (f && f[0] == 'w' && max_blk_len < 65536) return 2;
+  if (f && (f[0] == 'w' || f[0] == 'o') && max_blk_len < 65536) return 2;  // wsc / one-pass
   if (f && f[0] == 'l') return 1;
   if (f && f[0] == 'r' && max_blk_len <= 4096) return 0;
   // walk-scan-copy is three launches (walk, scan, copy): it wins from ~1k blocks up; small

@@ -114,9 +114,13 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     if (t == ntiles - 1) atomicExch(p.gcnt, 0u);  // every ticket is taken
     s_tile = t;
   }
-  if (p.zero_result && blockIdx.x == 0 && tid < 8) p.result[tid] = 0;  // see api.hip
   __syncthreads();
   const uint32_t tile = s_tile;
+  // the result block is zeroed by the workgroup holding ticket 0 (see api.hip), before anything
+  // else: every other tile's look-back ends only on a record chained to tile 0's, so no flag
+  // (the look-back timeout, result[5] |= 2) can be set before this and then erased
+  if (p.zero_result && tile == 0 && tid < 8)
+    atomicExch(reinterpret_cast<unsigned long long*>(p.result + tid), 0ull);
   // thread t owns block tile * TB + t (threads past TB own none: zero entries)
   const uint32_t b = tid < TB ? tile * TB + tid : 0xffffffffu;
   uint32_t n = 0, K = 0, V = 0, st = LSMGPU_BLK_OK;

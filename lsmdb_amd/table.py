@@ -22,13 +22,14 @@ from .codec import Codec, HostDecoded, default_codec, parse_index
 from .y import MAX_U64, ValueStruct, assert_true, compare_keys, parse_key
 
 RESULT_INTERVAL = 100  # table/builder.go:13-15 resultInterval
-# Finish's bloom tail: "bbloom" = the restated bbloom filter built on the device (default);
-# "all_ones" = every bit set, so a Go reader's DoesNotHave never skips the table.  The
-# restated bbloom bytes are parity unpinned (DESIGN.md "Bloom tail"): files a Go reader opens
-# should use "all_ones" (LSMDB_AMD_BLOOM=all_ones) until they are checked against Go.
+# Finish's bloom tail: "all_ones" (default) = every bit set, so a Go reader's DoesNotHave never
+# skips the table -- always correct, whatever bbloom's exact bytes are; "bbloom" = the restated
+# bbloom filter built on the device (Builder(bloom="bbloom") or LSMDB_AMD_BLOOM=bbloom).  The
+# restated bbloom bytes are parity unpinned (DESIGN.md "Bloom tail"), so the
+# default stays all-ones until they are checked against Go.
 BLOOM_BBLOOM = "bbloom"
 BLOOM_ALL_ONES = "all_ones"
-DEFAULT_BLOOM = os.environ.get("LSMDB_AMD_BLOOM", BLOOM_BBLOOM)
+DEFAULT_BLOOM = os.environ.get("LSMDB_AMD_BLOOM", BLOOM_ALL_ONES)
 MAX_U32 = 0xFFFFFFFF
 FILE_SUFFIX = ".sst"
 
@@ -315,7 +316,11 @@ def _read_index(t: Table, decoder) -> None:
     try:  # table.go:186 bbloom.JSONUnmarshal at open time
         t._bloom = _bloom.parse(t.bloom_json)
     except ValueError:
-        t._bloom = None  # a tail the restated parser cannot load: Has() = true (never skip)
+        # Deliberate divergence: Go's bbloom.JSONUnmarshal ignores JSON errors and builds a
+        # filter from whatever it parsed (so a Go reader may skip such a table); the exact
+        # lenient result is parity unpinned (no bbloom source here).  A tail the restated parser
+        # cannot load is treated as Has() = true: never skip, never a wrong miss.
+        t._bloom = None
     data_end = int(off[-1] + ln[-1]) if off.size else 0
     t.dec = decoder(np.frombuffer(raw, np.uint8)[:data_end] if data_end
                     else np.zeros(16, np.uint8), off, ln)
@@ -360,6 +365,9 @@ class BlockIterator:
             self.hpos = np.zeros(0, np.int64)
             self.stop = 0
         self.idx_of = {int(p): i for i, p in enumerate(self.hpos)}
+        # the decode stopped at a header Go cannot parse: reaching it panics there (a header
+        # slice past the block, or baseKey[:plen] past the base key -- iterator.go:96,121)
+        self.panics = int(d.blk_status[fb]) in (3, 4)  # BLK_TRUNC_HEADER, BLK_PREFIX_OOB
         self.Reset()
 
     # raw header field `prev` at block-relative position p (builder.go:23-43)
@@ -432,6 +440,8 @@ class BlockIterator:
             # the terminator (or the header the decode stopped at): itr.last = h, io.EOF
             if self.pos != self.stop:
                 raise TableError("cursor left the decoded entry chain")
+            if self.panics:
+                raise TableError("Go panics on this header (truncated, or plen past the base key)")
             self.last_pos = self.pos
             self.last_prev = self._prev_at(self.pos)
             self.pos += 10

@@ -139,9 +139,33 @@ def config_columns(cfg: int, n: int, seed_offset: int = 0) -> Columns:
 
 
 def entries_for_bytes(cfg: int, target_bytes: int) -> int:
-    """Entry count giving about target_bytes of block data for a config."""
-    per = {1: 130, 2: 130, 3: 1102, 4: 130, 5: 150}[cfg]
-    return max(1, target_bytes // per)
+    """An entry count giving at least target_bytes of block data for a config (an over-estimate:
+    the per-entry sizes below are under the generators' means -- C2 ~125.8 B with its
+    terminators, C3 ~1,105 B, C5 ~216 B; trim_to_bytes trims to the exact byte target)."""
+    per = {1: 118, 2: 118, 3: 1050, 4: 118, 5: 190}[cfg]
+    return max(1, target_bytes // per + 64)
 
 
-__all__ = ["Columns", "config_columns", "hex_keys", "encode_values", "entries_for_bytes"]
+def data_len_prefix(key_end: np.ndarray, vs_end: np.ndarray, plan: np.ndarray) -> np.ndarray:
+    """Block-data bytes of the first e entries, e = 1..n (Builder: 10-B header + key + vs per
+    entry, a 13-B terminator per block; plan = first entry of each block + end sentinel)."""
+    e = np.arange(1, key_end.size + 1, dtype=np.int64)
+    nblk = np.searchsorted(plan[:-1].astype(np.int64), e - 1, side="right")
+    return 10 * e + key_end.astype(np.int64) + vs_end.astype(np.int64) + 13 * nblk
+
+
+def trim_to_bytes(cols: Columns, plan: np.ndarray, target_bytes: int) -> Columns:
+    """The shortest prefix of cols whose block data reaches target_bytes (Builder's cut rule is
+    greedy, so the prefix's plan is the prefix of the plan)."""
+    dl = data_len_prefix(cols.key_end, cols.vs_end, plan)
+    idx = np.nonzero(dl >= target_bytes)[0]
+    if idx.size == 0:
+        raise ValueError(f"columns hold {int(dl[-1])} B < target {target_bytes} B")
+    n = int(idx[0]) + 1
+    kt, vt = int(cols.key_end[n - 1]), int(cols.vs_end[n - 1])
+    return Columns(cols.keys[:kt], cols.key_end[:n], cols.vs[:vt], cols.vs_end[:n],
+                   cols.entries_per_block, cols.block_bytes)
+
+
+__all__ = ["Columns", "config_columns", "hex_keys", "encode_values", "entries_for_bytes",
+           "data_len_prefix", "trim_to_bytes"]

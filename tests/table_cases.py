@@ -55,8 +55,8 @@ class GpuEnv:
 
     def build_bytes(self, kvs) -> bytes:
         kvs = sorted(kvs, key=lambda kv: kv[0])
-        b = T.NewTableBuilder()
-        b._codec = self.codec
+        # the device bbloom tail (Builder's default is all-ones): byte-compared with the oracle
+        b = T.Builder(bloom=T.BLOOM_BBLOOM, codec=self.codec)
         for k, v in kvs:
             b.Add(key_with_ts(k.encode(), 0), ValueStruct(meta=ord("A"), user_meta=0,
                                                           value=v.encode()))

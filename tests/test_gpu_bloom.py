@@ -91,7 +91,7 @@ def test_table_doesnothave_roundtrip(codec, tmp_path):
     probes ParseKey(key)) never rejects a present key."""
     from lsmdb_amd import table as T
     from lsmdb_amd.y import ValueStruct
-    b = T.NewTableBuilder()
+    b = T.Builder(bloom=T.BLOOM_BBLOOM, codec=codec)
     keys = [key_with_ts(b"user%06d" % i, 1) for i in range(0, 3000, 2)]
     for k in keys:
         b.Add(k, ValueStruct(meta=0x41, value=b"v" * 20))

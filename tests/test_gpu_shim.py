@@ -197,6 +197,89 @@ def _bottom_run(oracle, nt, per):
     return out
 
 
+def _go_compaction(oracle, ssts, run_first, cap):
+    """compactBuildTables (levels.go:239-283) run by the host mirror of the reference's own
+    iterator state machines (lsmdb_amd/table.py: OpenTable, Iterator, ConcatIterator;
+    lsmdb_amd/y.py: MergeIterator) over the ORACLE decode, then the oracle Builder loop.  Every
+    run is a ConcatIterator (one table behaves as its Iterator).  Returns None where Go panics
+    or log.Fatal()s (AssertTrue, a slice out of range, Decode of a nil value)."""
+    from lsmdb_amd import table as T, y
+    from test_gpu_compaction import _oracle_tables
+    try:
+        tables = [T.OpenTable(s, decoder=oracle.decode) for s in ssts]
+        iters = [T.ConcatIterator(tables[a:b]) for a, b in zip(run_first[:-1], run_first[1:])]
+        it = y.MergeIterator(iters)
+        it.Rewind()
+        ks, vs = [], []
+        while it.Valid():
+            k, v = it.Key(), it.Value()  # Value() of a nil block value panics (Decode)
+            ks.append(bytes(k))
+            vs.append(v.encode())
+            it.Next()
+    except (AssertionError, IndexError, TypeError, T.TableError):
+        return None
+    return _oracle_tables(oracle, ks, vs, cap, False)
+
+
+def _table_of(blocks):
+    data = b"".join(blocks)
+    return C.with_tail(data, np.cumsum([len(b) for b in blocks]).astype(np.uint32))
+
+
+def _good_blocks(oracle, lo, hi, step=1):
+    """Blocks of one Builder table over workload keys [lo, hi) (100 entries per block)."""
+    c = workload.config_columns(4, hi, seed_offset=3)
+    keys = [bytes(c.keys[(c.key_end[i - 1] if i else 0): c.key_end[i]]) for i in range(lo, hi, step)]
+    vss = [bytes(c.vs[(c.vs_end[i - 1] if i else 0): c.vs_end[i]]) for i in range(lo, hi, step)]
+    sst = oracle.build(keys, vss, entries_per_block=100)[0] + C.TAIL
+    off, ln, _, _ = oracle.parse_index(sst)
+    return [sst[int(o): int(o) + int(n)] for o, n in zip(off, ln)]
+
+
+def _overflow_first(block: bytes) -> bytes:
+    """The block with its first entry's vlen raised past the block end (a value overflow at
+    entry 0: Go's blockIterator stops with "Value exceeded size of block")."""
+    b = bytearray(block)
+    b[4:6] = (0xFFF0).to_bytes(2, "big")
+    return bytes(b)
+
+
+def test_shim_compact_corrupt_first_entries(codec, oracle):
+    """Go's iterator reachability on corrupt inputs: a table whose first block
+    yields nothing is dropped (seekToFirst invalid); as the first table of a ConcatIterator run
+    it drops the whole run; a later block that yields nothing is a Go crash (ERR_CORRUPT).
+    Expected values come from the host mirror of the Go iterators over the oracle decode."""
+    good = lambda lo, hi: _table_of(_good_blocks(oracle, lo, hi))
+    tb = _good_blocks(oracle, 0, 400, 2)          # 2 blocks of 100 entries (even keys)
+    bad_first = _table_of([_overflow_first(tb[0]), tb[1]])      # block 0 yields nothing
+    bad_later = _table_of([tb[0], _overflow_first(tb[1])])      # block 1 yields nothing
+    empty_tbl = oracle.build([], [], 100)[0] + C.TAIL           # one terminator-only block
+    no_blocks = b"\0\0\0\0" + C.TAIL                          # restarts count 0: no blocks
+    cases = {
+        # L0 shape: three top tables, one bottom run of two disjoint tables
+        "top_first_overflow": ([bad_first, good(1, 300), good(300, 600), good(600, 900)], [0, 1, 2, 4]),
+        "bottom_first_overflow": ([good(1, 300), bad_first, good(600, 900)], [0, 1, 3]),
+        "bottom_second_overflow": ([good(1, 300), good(0, 200), bad_first], [0, 1, 3]),
+        "bottom_first_empty": ([good(1, 300), empty_tbl, good(600, 900)], [0, 1, 3]),
+        "bottom_first_no_blocks": ([good(1, 300), no_blocks, good(600, 900)], [0, 1, 3]),
+        "top_empty": ([empty_tbl, good(0, 300)], [0, 1, 2]),
+        "later_block_overflow": ([bad_later, good(1, 300)], [0, 1, 2]),
+        "later_block_overflow_in_dropped_run": ([good(1, 300), empty_tbl, bad_later], [0, 1, 3]),
+    }
+    for name, (ssts, rf) in cases.items():
+        want = _go_compaction(oracle, ssts, rf, 1 << 20)
+        if want is None:
+            with pytest.raises(_lib.LsmgpuError) as e:
+                codec.compact_host(ssts, rf, 1 << 20)
+            assert e.value.code == _lib.ERR_CORRUPT, name
+        else:
+            got = codec.compact_host(ssts, rf, 1 << 20)
+            assert got == want, name
+    # the mirror agrees with the analysis for the cases that define the rules
+    assert _go_compaction(oracle, *cases["later_block_overflow"], 1 << 20) is None
+    assert _go_compaction(oracle, *cases["bottom_first_overflow"], 1 << 20) is not None
+
+
 def test_shim_compact_empty_and_corrupt(codec, oracle):
     L = _lib.lib()
     empty = oracle.build([], [], 100)[0] + C.TAIL
