@@ -123,6 +123,14 @@ int lsmgpu_decode_blocks(lsmgpu_ctx* ctx, const uint8_t* data, uint64_t data_len
                          int data_on_device, const uint32_t* blk_off, const uint32_t* blk_len,
                          uint64_t nblk, int mode, lsmgpu_decoded* out);
 
+/* Host-memory calls (data_on_device = 0) with blocks sorted by offset are pipelined: chunks of
+ * ~64 MiB (LSMGPU_HOST_CHUNK) are copied in, decoded and copied out on three streams at once.
+ * DMA runs at PCIe rate only from page-locked memory: pin the mmap'd .sst (and large output
+ * arrays) once with lsmgpu_host_register (hipHostRegister; read-only mappings accepted) and
+ * unpin with lsmgpu_host_unregister before munmap.  Memory already pinned is accepted. */
+int lsmgpu_host_register(lsmgpu_ctx* ctx, void* p, uint64_t bytes);
+int lsmgpu_host_unregister(lsmgpu_ctx* ctx, void* p);
+
 /* Device-resident asynchronous form (the benchmarked kernel): all pointers are device
  * pointers, max_blk_len bounds blk_len[] (selects the LDS slot), `d_result` (device, 8 u64)
  * receives {n_entries, key_bytes, val_bytes, first_bad_block+1, n_bad_blocks, flags, 0, 0}

@@ -71,6 +71,8 @@ EXPORTED_SYMBOLS = (
     "lsmgpu_compact_tables",
     "lsmgpu_compact_result",
     "lsmgpu_stream_probe_async",
+    "lsmgpu_host_register",
+    "lsmgpu_host_unregister",
 )
 
 COMPACT_BLOOM = 1
@@ -247,6 +249,10 @@ def _load() -> ctypes.CDLL:
     lib.lsmgpu_compact_tables.restype = c_int
     lib.lsmgpu_compact_result.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p, c_uint64]
     lib.lsmgpu_compact_result.restype = c_int
+    lib.lsmgpu_host_register.argtypes = [c_void_p, c_void_p, c_uint64]
+    lib.lsmgpu_host_register.restype = c_int
+    lib.lsmgpu_host_unregister.argtypes = [c_void_p, c_void_p]
+    lib.lsmgpu_host_unregister.restype = c_int
     lib.lsmgpu_stream_probe_async.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_uint64,
                                               c_uint32]
     lib.lsmgpu_stream_probe_async.restype = c_int

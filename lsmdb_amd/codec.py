@@ -173,6 +173,14 @@ class Codec:
         check(lib().lsmgpu_stream_probe_async(self._ctx, kind, _ptr(src), _ptr(dst), nbytes,
                                               wg_per_cu), "stream_probe_async")
 
+    # -- page-locked host memory (DMA at PCIe rate for the host-buffer calls)
+    def host_register(self, arr) -> None:
+        """Pins a host numpy array (an mmap'd .sst, an output array) until host_unregister."""
+        check(lib().lsmgpu_host_register(self._ctx, _ptr(arr), arr.nbytes), "host_register")
+
+    def host_unregister(self, arr) -> None:
+        check(lib().lsmgpu_host_unregister(self._ctx, _ptr(arr)), "host_unregister")
+
     # -- decode, host buffers (table.Table path)
     def decode_host(self, data, blk_off: np.ndarray, blk_len: np.ndarray,
                     mode: int = MODE_MATERIALIZE | MODE_VIEW) -> HostDecoded:

@@ -75,6 +75,15 @@ struct lsmgpu_ctx {
   std::vector<uint64_t> cp_tbl_out;  // ntables + 1 image offsets of the last compaction
   uint64_t cp_bytes = 0;
   bool cp_valid = false;
+  // host-memory decode pipeline (lsmgpu_decode_blocks, data_on_device = 0): copy-in / copy-out
+  // streams, per-slot device buffers and events, pinned per-chunk result words
+  static constexpr int kSlots = 3;
+  hipStream_t s_in = nullptr, s_out = nullptr;
+  struct Slot {
+    DevBuf data, off, len, kd, ke, vd, ve, view, bf, bs, res;
+    hipEvent_t in_done = nullptr, dec_done = nullptr, out_done = nullptr;
+  } slot[kSlots];
+  uint64_t* h_chunk_res = nullptr;  // pinned, 8 u64 per slot
 };
 
 #define HIPC(x)                                   \
@@ -143,6 +152,18 @@ void lsmgpu_close(lsmgpu_ctx* c) {
                     &c->cp_mke, &c->cp_mve, &c->cp_tf, &c->cp_tb, &c->cp_to,
                     &c->cp_out, &c->cp_flags, &c->cp_scratch};
   for (DevBuf* b : bufs) b->release();
+  for (auto& sl : c->slot) {
+    DevBuf* sb[] = {&sl.data, &sl.off, &sl.len, &sl.kd, &sl.ke, &sl.vd, &sl.ve, &sl.view,
+                    &sl.bf, &sl.bs, &sl.res};
+    for (DevBuf* b : sb) b->release();
+    for (hipEvent_t* e : {&sl.in_done, &sl.dec_done, &sl.out_done})
+      if (*e) (void)hipEventDestroy(*e);
+  }
+  if (c->s_in) (void)hipStreamSynchronize(c->s_in);
+  if (c->s_out) (void)hipStreamSynchronize(c->s_out);
+  if (c->s_in) (void)hipStreamDestroy(c->s_in);
+  if (c->s_out) (void)hipStreamDestroy(c->s_out);
+  if (c->h_chunk_res) (void)hipHostFree(c->h_chunk_res);
   if (c->h_result) (void)hipHostFree(c->h_result);
   for (hipEvent_t& e : c->kev)
     if (e) (void)hipEventDestroy(e);
@@ -370,15 +391,232 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
   return LSMGPU_OK;
 }
 
+int lsmgpu_host_register(lsmgpu_ctx* c, void* p, uint64_t bytes) {
+  if (!c || !p || !bytes) return LSMGPU_ERR_ARG;
+  HIPC(hipSetDevice(c->device));
+  // read-only first (an mmap'd .sst is PROT_READ), then read-write memory
+  hipError_t e = hipHostRegister(p, bytes, hipHostRegisterPortable | hipHostRegisterReadOnly);
+  if (e != hipSuccess && e != hipErrorHostMemoryAlreadyRegistered) {
+    (void)hipGetLastError();
+    e = hipHostRegister(p, bytes, hipHostRegisterPortable);
+  }
+  if (e == hipErrorHostMemoryAlreadyRegistered) {
+    (void)hipGetLastError();
+    return LSMGPU_OK;
+  }
+  return e == hipSuccess ? LSMGPU_OK : LSMGPU_ERR_HIP;
+}
+
+int lsmgpu_host_unregister(lsmgpu_ctx* c, void* p) {
+  if (!c || !p) return LSMGPU_ERR_ARG;
+  HIPC(hipSetDevice(c->device));
+  HIPC(hipHostUnregister(p));
+  return LSMGPU_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// key_end / val_end / blk_first of one chunk of a pipelined host decode += the entries, key
+// bytes and value bytes of the chunks before it (the chunk was decoded with bases 0)
+__global__ void __launch_bounds__(256) add_bases_kernel(uint32_t* ke, uint32_t* ve, uint32_t n,
+                                                        uint32_t kb, uint32_t vb, uint32_t* bf,
+                                                        uint32_t nb1, uint32_t eb) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    if (ke) ke[i] += kb;
+    if (ve) ve[i] += vb;
+  }
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nb1; i += stride) bf[i] += eb;
+}
+
+constexpr int kNotPipelined = -1;
+
+// lsmgpu_decode_blocks for host memory, as a pipeline: the blocks (sorted by offset, disjoint)
+// are cut into chunks of ~64 MiB of input; chunk c's copy-in (s_in), decode (ctx stream) and
+// copy-out (s_out) overlap chunk c+1's copy-in and chunk c-1's copy-out, over kSlots device
+// slots.  Each chunk decodes with bases 0; once its decode has finished the host knows the
+// chunk's totals, adds the bases of the chunks before it on the device (add_bases_kernel) and
+// copies the outputs to their places.  Returns kNotPipelined when the batch is one chunk, the
+// blocks are unsorted or a chunk overflows its device slot (prefix-compressed keys that expand):
+// the caller then decodes in one shot.
+int decode_host_pipelined(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
+                          const uint32_t* blk_off, const uint32_t* blk_len, uint64_t nblk,
+                          int mode, lsmgpu_decoded* out, uint32_t max_len) {
+  const char* ch_env = getenv("LSMGPU_HOST_CHUNK");
+  const uint64_t chunk = ch_env && atoll(ch_env) >= (1 << 20) ? (uint64_t)atoll(ch_env) : (64ull << 20);
+  if (max_len >= 65536 || nblk < 2) return kNotPipelined;
+  for (uint64_t b = 0; b < nblk; b++) {
+    if ((uint64_t)blk_off[b] + blk_len[b] > data_len) return kNotPipelined;
+    if (b && blk_off[b] < (uint64_t)blk_off[b - 1] + blk_len[b - 1]) return kNotPipelined;
+  }
+  std::vector<uint64_t> cb{0};  // chunk c = blocks [cb[c], cb[c+1])
+  for (uint64_t b = 1; b < nblk; b++)
+    if ((uint64_t)blk_off[b] + blk_len[b] - blk_off[cb.back()] > chunk) cb.push_back(b);
+  cb.push_back(nblk);
+  const uint64_t nch = cb.size() - 1;
+  if (nch < 2) return kNotPipelined;
+  uint64_t max_span = 0, max_nb = 0;
+  for (uint64_t k = 0; k < nch; k++) {
+    const uint64_t a = blk_off[cb[k]] & ~127ull, e = (uint64_t)blk_off[cb[k + 1] - 1] + blk_len[cb[k + 1] - 1];
+    max_span = std::max(max_span, e - a);
+    max_nb = std::max(max_nb, cb[k + 1] - cb[k]);
+  }
+  const bool mat = (mode & LSMGPU_MODE_MATERIALIZE) != 0, view = (mode & LSMGPU_MODE_VIEW) != 0;
+  const uint64_t ecap = max_span / 10 + 1;  // >= 10 B per entry (its header)
+  if (!c->s_in) HIPC(hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking));
+  if (!c->s_out) HIPC(hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking));
+  if (!c->h_chunk_res)
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->h_chunk_res), 64 * lsmgpu_ctx::kSlots,
+                       hipHostMallocDefault));
+  for (auto& sl : c->slot) {
+    HIPC(sl.data.ensure(max_span + 256));
+    HIPC(sl.off.ensure(max_nb * 4 + 4));
+    HIPC(sl.len.ensure(max_nb * 4 + 4));
+    HIPC(sl.bf.ensure(max_nb * 4 + 8));
+    HIPC(sl.bs.ensure(max_nb * 4 + 4));
+    HIPC(sl.res.ensure(64));
+    if (mat) {
+      HIPC(sl.kd.ensure(max_span + 16));
+      HIPC(sl.vd.ensure(max_span + 16));
+      HIPC(sl.ke.ensure(ecap * 4));
+      HIPC(sl.ve.ensure(ecap * 4));
+    }
+    if (view) HIPC(sl.view.ensure(ecap * 8));
+    for (hipEvent_t* e : {&sl.in_done, &sl.dec_done, &sl.out_done})
+      if (!*e) HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  }
+  // running totals of the chunks already placed
+  uint64_t E = 0, KB = 0, VB = 0, nbad = 0;
+  int64_t first_bad = -1;
+  bool fits = true;
+  std::vector<uint8_t> slot_used(lsmgpu_ctx::kSlots, 0);
+  auto drain = [&]() {
+    (void)hipStreamSynchronize(c->s_in);
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->s_out);
+  };
+  for (uint64_t i = 0; i <= nch; i++) {
+    if (i < nch) {  // chunk i: copy in, decode
+      auto& sl = c->slot[i % lsmgpu_ctx::kSlots];
+      const uint64_t b0 = cb[i], nb = cb[i + 1] - b0;
+      const uint64_t a = blk_off[b0] & ~127ull, e = (uint64_t)blk_off[cb[i + 1] - 1] + blk_len[cb[i + 1] - 1];
+      if (slot_used[i % lsmgpu_ctx::kSlots]) HIPC(hipStreamWaitEvent(c->s_in, sl.out_done, 0));
+      slot_used[i % lsmgpu_ctx::kSlots] = 1;
+      HIPC(hipMemcpyAsync(sl.data.p, data + a, e - a, hipMemcpyHostToDevice, c->s_in));
+      HIPC(hipMemcpyAsync(sl.off.p, blk_off + b0, nb * 4, hipMemcpyHostToDevice, c->s_in));
+      HIPC(hipMemcpyAsync(sl.len.p, blk_len + b0, nb * 4, hipMemcpyHostToDevice, c->s_in));
+      HIPC(hipEventRecord(sl.in_done, c->s_in));
+      HIPC(hipStreamWaitEvent(c->stream, sl.in_done, 0));
+      lsmgpu_decoded d{};
+      if (mat) {
+        d.key_data = sl.kd.as<uint8_t>();
+        d.key_cap = max_span;
+        d.key_end = sl.ke.as<uint32_t>();
+        d.val_data = sl.vd.as<uint8_t>();
+        d.val_cap = max_span;
+        d.val_end = sl.ve.as<uint32_t>();
+      }
+      if (view) d.view = sl.view.as<uint64_t>();
+      d.ent_cap = ecap;
+      d.blk_first = sl.bf.as<uint32_t>();
+      d.blk_status = sl.bs.as<int32_t>();
+      uint32_t ml = 0;
+      for (uint64_t b = b0; b < b0 + nb; b++) ml = std::max(ml, blk_len[b]);
+      // the slot holds data[a, e): the kernels see it through a pointer biased by -a, so the
+      // caller's offsets (and the view records' key positions) stay absolute
+      int rc = lsmgpu_decode_blocks_async(c, sl.data.as<uint8_t>() - a, e,
+                                          sl.off.as<uint32_t>(), sl.len.as<uint32_t>(), nb, ml,
+                                          mode, &d, sl.res.as<uint64_t>());
+      if (rc != LSMGPU_OK) {
+        drain();
+        return rc;
+      }
+      HIPC(hipMemcpyAsync(c->h_chunk_res + 8 * (i % lsmgpu_ctx::kSlots), sl.res.p, 64,
+                          hipMemcpyDeviceToHost, c->stream));
+      HIPC(hipEventRecord(sl.dec_done, c->stream));
+    }
+    if (i == 0) continue;
+    // chunk j = i - 1: its totals, then the bases and the copy-out
+    const uint64_t j = i - 1, b0 = cb[j], nb = cb[j + 1] - b0;
+    auto& sl = c->slot[j % lsmgpu_ctx::kSlots];
+    HIPC(hipEventSynchronize(sl.dec_done));
+    const uint64_t* r = c->h_chunk_res + 8 * (j % lsmgpu_ctx::kSlots);
+    const uint64_t n = r[0], kb = r[1], vb = r[2], fb = r[3], bad = r[4], fl = r[5];
+    if (fl & 2) {
+      drain();
+      return LSMGPU_ERR_INTERNAL;
+    }
+    if (fl & 1) {  // a chunk outgrew its slot (expanding prefix-compressed keys)
+      drain();
+      return kNotPipelined;
+    }
+    if (fb && first_bad < 0) first_bad = (int64_t)(b0 + nb - fb);
+    nbad += bad;
+    fits = fits && E + n <= out->ent_cap && E + n <= 0xffffffffull &&
+           (!out->key_data || KB + kb <= out->key_cap) && (!out->val_data || VB + vb <= out->val_cap) &&
+           KB + kb < 0xffffffffull && VB + vb <= 0xffffffffull;
+    HIPC(hipStreamWaitEvent(c->s_out, sl.dec_done, 0));
+    const bool last = j + 1 == nch;
+    if (E | KB | VB) {
+      const uint32_t nb1 = (uint32_t)nb + (last ? 1 : 0);
+      hipLaunchKernelGGL(add_bases_kernel, dim3(512), dim3(256), 0, c->s_out,
+                         mat && fits && out->key_end ? sl.ke.as<uint32_t>() : nullptr,
+                         mat && fits && out->val_end ? sl.ve.as<uint32_t>() : nullptr,
+                         fits ? (uint32_t)n : 0u, (uint32_t)KB, (uint32_t)VB, sl.bf.as<uint32_t>(),
+                         out->blk_first ? nb1 : 0u, (uint32_t)E);
+      HIPC(hipGetLastError());
+    }
+    auto back = [&](void* hp, const void* dp, uint64_t bytes) -> hipError_t {
+      if (!hp || !bytes) return hipSuccess;
+      return hipMemcpyAsync(hp, dp, bytes, hipMemcpyDeviceToHost, c->s_out);
+    };
+    if (fits) {
+      if (mat) {
+        HIPC(back(out->key_data ? out->key_data + KB : nullptr, sl.kd.p, kb));
+        HIPC(back(out->val_data ? out->val_data + VB : nullptr, sl.vd.p, vb));
+        HIPC(back(out->key_end ? out->key_end + E : nullptr, sl.ke.p, n * 4));
+        HIPC(back(out->val_end ? out->val_end + E : nullptr, sl.ve.p, n * 4));
+      }
+      if (view) HIPC(back(out->view ? out->view + E : nullptr, sl.view.p, n * 8));
+    }
+    HIPC(back(out->blk_first ? out->blk_first + b0 : nullptr, sl.bf.p, (nb + (last ? 1 : 0)) * 4));
+    HIPC(back(out->blk_status ? out->blk_status + b0 : nullptr, sl.bs.p, nb * 4));
+    HIPC(hipEventRecord(sl.out_done, c->s_out));
+    E += n;
+    KB += kb;
+    VB += vb;
+  }
+  HIPC(hipStreamSynchronize(c->s_out));
+  out->n_entries = E;
+  out->key_bytes = KB;
+  out->val_bytes = VB;
+  out->first_bad_block = first_bad;
+  out->n_bad_blocks = nbad;
+  return fits ? LSMGPU_OK : LSMGPU_ERR_CAPACITY;
+}
+
+}  // namespace
+
+extern "C" {
+
 int lsmgpu_decode_blocks(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
                          int data_on_device, const uint32_t* blk_off, const uint32_t* blk_len,
                          uint64_t nblk, int mode, lsmgpu_decoded* out) {
   if (!c || !out) return LSMGPU_ERR_ARG;
   if (nblk && (!blk_off || !blk_len || !data)) return LSMGPU_ERR_ARG;
   if (data_len > 0xffffffffull) return LSMGPU_ERR_TOO_LARGE;
+  if (mode & ~(LSMGPU_MODE_MATERIALIZE | LSMGPU_MODE_VIEW)) return LSMGPU_ERR_ARG;
   HIPC(hipSetDevice(c->device));
   uint32_t max_len = 0;
   for (uint64_t b = 0; b < nblk; b++) max_len = std::max(max_len, blk_len[b]);
+  const bool query0 = !out->key_data && !out->key_end && !out->val_data && !out->val_end &&
+                      !out->view && !out->blk_first && !out->blk_status;
+  if (!data_on_device && !query0) {  // host memory: the chunked copy-in / decode / copy-out pipeline
+    const int prc = decode_host_pipelined(c, data, data_len, blk_off, blk_len, nblk, mode, out, max_len);
+    if (prc != kNotPipelined) return prc;
+  }
   HIPC(c->s_off.ensure((nblk + 1) * 4));
   HIPC(c->s_len.ensure((nblk + 1) * 4));
   if (nblk) {

@@ -1,0 +1,168 @@
+"""End-to-end decode through the C ABI from host memory (SURVEY §8(d) "End-to-end"; the drop-in
+path of an mmap'd .sst, table/table.go:88-144,153-166): lsmgpu_decode_blocks with
+data_on_device = 0 over the C2 1 GiB shard held in page-locked host memory
+(lsmgpu_host_register, what a cgo caller does to its mmap), outputs in registered host arrays.
+The library pipelines chunks (copy-in / decode / copy-out on three streams).  Reported beside the
+PCIe bound measured on the same box with the same buffers: hipMemcpyAsync of the input H2D, of
+the outputs D2H, and both at once on two streams.  The outputs are checked against a
+device-resident decode of the same blocks.  Prints one JSON line.
+
+    python scripts/e2e_abi.py [--reps N] [--chunk-mib M]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+from ctypes import byref
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+H2D, D2H = 1, 2  # hipMemcpyKind
+
+
+def hip_runtime():
+    """The HIP runtime the library is bound to (torch's libamdhip64, see lsmdb_amd/_lib.py)."""
+    import torch
+    path = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+    rt = ctypes.CDLL(path if os.path.exists(path) else "libamdhip64.so")
+    rt.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                  ctypes.c_void_p]
+    rt.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    return rt
+
+
+def median_s(fn, reps):
+    fn()  # warm-up
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--chunk-mib", type=int, default=0)
+    args = ap.parse_args()
+    if args.chunk_mib:
+        os.environ["LSMGPU_HOST_CHUNK"] = str(args.chunk_mib << 20)
+    import torch
+    import bench
+    from lsmdb_amd import _lib
+    from lsmdb_amd.codec import Codec, MODE_MATERIALIZE, MODE_VIEW, _ptr
+    dev = torch.device("cuda", 0)
+    codec = Codec(0)
+    w = bench.build_device_sst(codec, torch, dev, 2, 1 << 30, 0)
+    data_len, n, nblk = w["data_len"], w["n"], w["nblocks"]
+    kt, vt = w["key_total"], w["vs_total"]
+    off = np.ascontiguousarray(w["offs"], np.uint32)
+    ln = np.ascontiguousarray(w["lens"], np.uint32)
+    host = np.empty(data_len, np.uint8)
+    host[:] = w["d_sst"][:data_len].cpu().numpy()
+    ref = codec.alloc_decode(data_len, data_len, nblk, MODE_MATERIALIZE | MODE_VIEW, ent_cap=n)
+    codec.decode_device_async(w["d_sst"], w["d_off"], w["d_len"], w["max_len"],
+                              MODE_MATERIALIZE | MODE_VIEW, ref, data_len=data_len)
+    torch.cuda.synchronize()
+    want = dict(view=ref.view[:n].cpu().numpy().view(np.uint64),
+                ke=ref.key_end[:n].cpu().numpy().view(np.uint32),
+                ve=ref.val_end[:n].cpu().numpy().view(np.uint32),
+                kd=ref.key_data[:kt].cpu().numpy(), vd=ref.val_data[:vt].cpu().numpy(),
+                bf=ref.blk_first[: nblk + 1].cpu().numpy().view(np.uint32))
+    del ref, w
+    torch.cuda.empty_cache()
+
+    # the caller's buffers, page-locked once (an mmap'd .sst would be registered read-only)
+    ecap = data_len // 10 + 1
+    outs = dict(kd=np.empty(data_len, np.uint8), vd=np.empty(data_len, np.uint8),
+                ke=np.empty(ecap, np.uint32), ve=np.empty(ecap, np.uint32),
+                view=np.empty(ecap, np.uint64), bf=np.empty(nblk + 1, np.uint32),
+                bs=np.empty(nblk, np.int32))
+    t0 = time.perf_counter()
+    codec.host_register(host)
+    for a in outs.values():
+        codec.host_register(a)
+    reg_s = time.perf_counter() - t0
+    L = _lib.lib()
+
+    def decode(mode):
+        d = _lib.LsmgpuDecoded()
+        mat = mode & MODE_MATERIALIZE
+        d.key_data, d.key_cap = (_ptr(outs["kd"]), data_len) if mat else (None, 0)
+        d.val_data, d.val_cap = (_ptr(outs["vd"]), data_len) if mat else (None, 0)
+        d.key_end = _ptr(outs["ke"]) if mat else None
+        d.val_end = _ptr(outs["ve"]) if mat else None
+        d.view = _ptr(outs["view"]) if mode & MODE_VIEW else None
+        d.ent_cap, d.blk_first, d.blk_status = ecap, _ptr(outs["bf"]), _ptr(outs["bs"])
+        rc = L.lsmgpu_decode_blocks(codec._ctx, _ptr(host), data_len, 0, _ptr(off), _ptr(ln), nblk,
+                                    mode, byref(d))
+        assert rc == _lib.OK, rc
+        assert d.n_entries == n
+        return d
+
+    res = {}
+    for name, mode in (("view", MODE_VIEW), ("materialize", MODE_MATERIALIZE)):
+        s = median_s(lambda: decode(mode), args.reps)
+        if mode & MODE_VIEW:
+            assert np.array_equal(outs["view"][:n], want["view"]), "view parity"
+        else:
+            assert np.array_equal(outs["ke"][:n], want["ke"]) and np.array_equal(outs["ve"][:n], want["ve"])
+            assert np.array_equal(outs["kd"][:kt], want["kd"]) and np.array_equal(outs["vd"][:vt], want["vd"])
+        assert np.array_equal(outs["bf"], want["bf"]), "blk_first parity"
+        back = n * 8 + nblk * 8 if mode & MODE_VIEW else kt + vt + 8 * n + nblk * 8
+        res[name] = dict(seconds=round(s, 5), input_gibs=round(data_len / s / (1 << 30), 2),
+                         bytes_in=data_len, bytes_out=back)
+
+    # the PCIe bound with the same registered buffers (a device buffer of the input's size)
+    rt = hip_runtime()
+    dbuf = torch.empty(data_len, dtype=torch.uint8, device=dev)
+    dout = torch.empty(data_len, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def copy(kind, dst, src, nbytes, stream):
+        assert rt.hipMemcpyAsync(dst, src, nbytes, kind, stream.cuda_stream) == 0
+
+    def h2d():
+        copy(H2D, dbuf.data_ptr(), _ptr(host), data_len, s1)
+        rt.hipStreamSynchronize(s1.cuda_stream)
+
+    def d2h(nbytes):
+        def f():
+            copy(D2H, _ptr(outs["kd"]), dout.data_ptr(), nbytes, s2)
+            rt.hipStreamSynchronize(s2.cuda_stream)
+        return f
+
+    def both(nbytes):
+        def f():
+            copy(H2D, dbuf.data_ptr(), _ptr(host), data_len, s1)
+            copy(D2H, _ptr(outs["kd"]), dout.data_ptr(), nbytes, s2)
+            rt.hipStreamSynchronize(s1.cuda_stream)
+            rt.hipStreamSynchronize(s2.cuda_stream)
+        return f
+
+    t_h2d = median_s(h2d, args.reps)
+    for name in res:
+        nb = min(res[name]["bytes_out"], data_len)
+        bound = max(t_h2d, median_s(both(nb), args.reps))
+        res[name]["pcie_bound_s"] = round(bound, 5)
+        res[name]["frac_of_pcie_bound"] = round(bound / res[name]["seconds"], 4)
+    res["pcie"] = dict(h2d_gbs=round(data_len / t_h2d / 1e9, 2),
+                       d2h_gbs=round(data_len / median_s(d2h(data_len), args.reps) / 1e9, 2),
+                       host_register_s=round(reg_s, 3))
+    codec.host_unregister(host)
+    for a in outs.values():
+        codec.host_unregister(a)
+    print(json.dumps({"what": "E2E decode through lsmgpu_decode_blocks (data_on_device=0), C2 "
+                      f"{data_len} B, {nblk} blocks, {n} entries; host buffers registered; "
+                      "chunk " + os.environ.get("LSMGPU_HOST_CHUNK", "64 MiB default"),
+                      **res}), flush=True)
+    codec.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,8 +1,9 @@
 """The cgo shim's exact call sequences, replayed through ctypes on the GPU:
 
-* decodeTable: parse_index size query -> allocate -> parse_index; decode size query (every output
-  pointer NULL) -> newDecodedBatch with the reported needs -> decode_blocks.  Checked against the
-  oracle's decode of the same blocks (table/iterator.go:93-135).
+* decodeTable: parse_index size query -> allocate -> parse_index; newDecodedBatch with upper
+  bounds -> decode_blocks (-> the reported needs and a second decode_blocks only on
+  LSMGPU_ERR_CAPACITY); optionally pinned first (pinMmap).  Checked against the oracle's decode
+  of the same blocks (table/iterator.go:93-135).
 * finishBlocks: encode_blocks size query (out == NULL) -> allocate out_len -> encode_blocks.
   Checked byte for byte against the oracle Builder (table/builder.go:84-198).
 * compactBuildTables: lsmgpu_compact_tables -> lsmgpu_compact_result, checked against the oracle
@@ -24,10 +25,14 @@ pytestmark = pytest.mark.gpu
 MAT_VIEW = _lib.MODE_MATERIALIZE | _lib.MODE_VIEW
 
 
-def shim_decode_table(ctx, sst: bytes):
-    """decodeTable step by step; returns the host SoA and the query result."""
+def shim_decode_table(ctx, sst: bytes, pin: bool = False):
+    """decodeTable step by step: tail parse, upper-bound buffers (entries <=
+    data/10, key and value bytes <= data), one decode; on LSMGPU_ERR_CAPACITY (prefix-compressed
+    keys that expand) the reported needs are allocated and the decode repeated.  pin: the
+    table's bytes page-locked first (pinMmap).  Returns the host SoA, the final call's needs,
+    the block list and the number of decode calls made."""
     L = _lib.lib()
-    base = np.frombuffer(sst + b"\0", np.uint8)
+    base = np.frombuffer(sst + b"\0", np.uint8).copy()
     nblk, bo, bl = c_uint64(0), c_uint64(0), c_uint64(0)
     rc = L.lsmgpu_parse_index(_ptr(base), len(sst), None, None, 0, byref(nblk), byref(bo), byref(bl))
     assert rc in (_lib.OK, _lib.ERR_CAPACITY)
@@ -37,27 +42,37 @@ def shim_decode_table(ctx, sst: bytes):
                                 byref(bo), byref(bl)) == _lib.OK
     n = nblk.value
     data_end = int(off[n - 1]) + int(ln[n - 1]) if n else 0
-    q = _lib.LsmgpuDecoded()  # every output pointer NULL: the size query
-    assert L.lsmgpu_decode_blocks(ctx, _ptr(base), data_end, 0, _ptr(off), _ptr(ln), n, MAT_VIEW,
-                                  byref(q)) == _lib.OK
-    need = (q.n_entries, q.key_bytes, q.val_bytes, q.first_bad_block, q.n_bad_blocks)
-    # newDecodedBatch(entries, keyBytes, valBytes, nblk, mode): exactly the reported needs
-    kd = np.zeros(max(q.key_bytes, 1), np.uint8)
-    vd = np.zeros(max(q.val_bytes, 1), np.uint8)
-    ke = np.zeros(max(q.n_entries, 1), np.uint32)
-    ve = np.zeros(max(q.n_entries, 1), np.uint32)
-    vw = np.zeros(max(q.n_entries, 1), np.uint64)
-    bf = np.zeros(n + 1, np.uint32)
-    bs = np.zeros(max(n, 1), np.int32)
-    d = _lib.LsmgpuDecoded()
-    d.key_data, d.key_cap, d.key_end = _ptr(kd), q.key_bytes, _ptr(ke)
-    d.val_data, d.val_cap, d.val_end = _ptr(vd), q.val_bytes, _ptr(ve)
-    d.view, d.ent_cap, d.blk_first, d.blk_status = _ptr(vw), q.n_entries, _ptr(bf), _ptr(bs)
-    assert L.lsmgpu_decode_blocks(ctx, _ptr(base), data_end, 0, _ptr(off), _ptr(ln), n, MAT_VIEW,
-                                  byref(d)) == _lib.OK
+    if pin:
+        assert L.lsmgpu_host_register(ctx, _ptr(base), base.size) == _lib.OK
+
+    def batch(entries, kbytes, vbytes):  # newDecodedBatch
+        arrs = dict(kd=np.zeros(max(kbytes, 1), np.uint8), vd=np.zeros(max(vbytes, 1), np.uint8),
+                    ke=np.zeros(max(entries, 1), np.uint32), ve=np.zeros(max(entries, 1), np.uint32),
+                    vw=np.zeros(max(entries, 1), np.uint64), bf=np.zeros(n + 1, np.uint32),
+                    bs=np.zeros(max(n, 1), np.int32))
+        d = _lib.LsmgpuDecoded()
+        d.key_data, d.key_cap, d.key_end = _ptr(arrs["kd"]), kbytes, _ptr(arrs["ke"])
+        d.val_data, d.val_cap, d.val_end = _ptr(arrs["vd"]), vbytes, _ptr(arrs["ve"])
+        d.view, d.ent_cap = _ptr(arrs["vw"]), entries
+        d.blk_first, d.blk_status = _ptr(arrs["bf"]), _ptr(arrs["bs"])
+        return d, arrs
+
+    calls = 1
+    d, arrs = batch(data_end // 10 + 1, data_end, data_end)
+    rc = L.lsmgpu_decode_blocks(ctx, _ptr(base), data_end, 0, _ptr(off), _ptr(ln), n, MAT_VIEW, byref(d))
+    if rc == _lib.ERR_CAPACITY:
+        calls += 1
+        d, arrs = batch(d.n_entries, d.key_bytes, d.val_bytes)
+        rc = L.lsmgpu_decode_blocks(ctx, _ptr(base), data_end, 0, _ptr(off), _ptr(ln), n, MAT_VIEW,
+                                    byref(d))
+    if pin:
+        assert L.lsmgpu_host_unregister(ctx, _ptr(base)) == _lib.OK
+    assert rc == _lib.OK
     m = d.n_entries
-    got = dict(n=m, kd=kd[: d.key_bytes].tobytes(), vd=vd[: d.val_bytes].tobytes(), ke=ke[:m],
-               ve=ve[:m], view=vw[:m], bf=bf, bs=bs[:n], fbb=d.first_bad_block, nbad=d.n_bad_blocks)
+    need = (d.n_entries, d.key_bytes, d.val_bytes, d.first_bad_block, d.n_bad_blocks)
+    got = dict(n=m, kd=arrs["kd"][: d.key_bytes].tobytes(), vd=arrs["vd"][: d.val_bytes].tobytes(),
+               ke=arrs["ke"][:m], ve=arrs["ve"][:m], view=arrs["vw"][:m], bf=arrs["bf"],
+               bs=arrs["bs"][:n], fbb=d.first_bad_block, nbad=d.n_bad_blocks, calls=calls)
     return got, need, off[:n], ln[:n]
 
 
@@ -82,20 +97,36 @@ def test_shim_decode_table(codec, oracle, cfg, n):
     else:
         body, _, _ = oracle.build([], [], 100)
     sst = body + C.TAIL
-    got, need, off, ln = shim_decode_table(codec._ctx, sst)
-    _check_against_oracle(oracle, sst, got, need, off, ln)
+    for pin in (False, True):
+        got, need, off, ln = shim_decode_table(codec._ctx, sst, pin=pin)
+        _check_against_oracle(oracle, sst, got, need, off, ln)
+        assert got["calls"] == 1  # one copy of the table: no size-query pass
+
+
+def test_shim_decode_table_pipelined(codec, oracle, monkeypatch):
+    """decodeTable on a table larger than several pipeline chunks (LSMGPU_HOST_CHUNK = 1 MiB),
+    pinned and not."""
+    monkeypatch.setenv("LSMGPU_HOST_CHUNK", str(1 << 20))
+    c = workload.config_columns(2, 120000)
+    body, _, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, c.entries_per_block,
+                                   c.block_bytes)
+    sst = body + C.TAIL
+    for pin in (False, True):
+        got, need, off, ln = shim_decode_table(codec._ctx, sst, pin=pin)
+        _check_against_oracle(oracle, sst, got, need, off, ln)
+        assert got["calls"] == 1
 
 
 def test_shim_decode_expanding_and_bad_blocks(codec, oracle):
-    """The query reports what prefix-compressed keys expand to (more key bytes than the input)
-    and the bad-block counts; the exact-size call then succeeds."""
+    """Prefix-compressed keys that expand past the input's size: the first call returns
+    LSMGPU_ERR_CAPACITY with the exact needs (and the bad-block counts), the second succeeds."""
     blocks = [K.PLEN_BLOCK] * 40 + [kat[1] for kat in K.DECODE_KATS]
     data = b"".join(blocks)
     ends = np.cumsum([len(b) for b in blocks]).astype(np.uint32)
     sst = C.with_tail(data, ends)
     got, need, off, ln = shim_decode_table(codec._ctx, sst)
     _check_against_oracle(oracle, sst, got, need, off, ln)
-    assert need[3] >= 0 and need[4] > 0
+    assert need[3] >= 0 and need[4] > 0 and got["calls"] == 2
 
 
 @pytest.mark.parametrize("cfg,n", [(1, 10000), (2, 20000), (3, 2000), (5, 10000), (1, 0)])
