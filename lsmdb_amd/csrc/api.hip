@@ -340,6 +340,8 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     const char* vf_env = getenv("LSMGPU_WSC_VIEWFUSE");
     const bool fuse = vf_env ? atoi(vf_env) != 0 : nblk >= 512ull * (uint64_t)c->num_cus;
     p.wfuse = !(mode & LSMGPU_MODE_MATERIALIZE) && fuse;
+    const char* ch_env = getenv("LSMGPU_WSC_CHUNK");  // lane walk: 16- or 32-record flushes
+    p.wchunk = ch_env && atoi(ch_env) == 16 ? 16u : 32u;
     const char* wk_env = getenv("LSMGPU_WSC_WALK");
     // Default: 8 lanes per block guessing same-shape runs (kWalkGroup) when the batch has at
     // most 64 blocks per CU -- one lane per block would leave the machine idle and the walk is
@@ -361,6 +363,10 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     const char* dp_env = getenv("LSMGPU_DECODE_PATH");
     const bool onepass_env = dp_env && strncmp(dp_env, "one", 3) == 0;
     if (onepass_env) {
+      const char* pf_env = getenv("LSMGPU_ONEPASS_PF");  // A/B: 0 = no line fetch before the walk
+      p.wprefetch = pf_env && atoi(pf_env) == 0 ? 0u : 1u;
+      const char* bt_env = getenv("LSMGPU_ONEPASS_BATCH");  // A/B: batched piece loads
+      p.wbatch = bt_env && atoi(bt_env) == 1 ? 1u : 0u;
       HIPC(hipMemsetAsync(d_result, 0, 8 * sizeof(uint64_t), c->stream));
       if (c->ktime) HIPC(hipEventRecord(c->kev[0], c->stream));
       HIPC(launch_decode_onepass(p, max_blk_len, c->num_cus, c->stream));

@@ -107,6 +107,96 @@ __device__ __forceinline__ void copy_bytes(const Rec& rec, const uint8_t* blk, u
   }
 }
 
+// the same, with every lane's first piece of each of the G entries loaded before any is stored
+// (one wait for the pass instead of a load -> store round trip per piece: the lines come from
+// L2 / the Infinity Cache, so the copy is latency-bound per worker); further pieces (entries
+// wider than J 16-B pieces) take the piecewise loop
+__device__ __forceinline__ void piece_at(const uint8_t* src, uint8_t* dst, uint32_t len, uint32_t q,
+                                         const uint8_t*& s, uint8_t*& d, uint32_t& w) {
+  if (len >= 16) {
+    const uint32_t o = min(16 * q, len - 16);
+    s = src + o; d = dst + o; w = 16;
+  } else if (len >= 8) {
+    const uint32_t o = q ? len - 8 : 0;
+    s = src + o; d = dst + o; w = 8;
+  } else if (len >= 4) {
+    const uint32_t o = q ? len - 4 : 0;
+    s = src + o; d = dst + o; w = 4;
+  } else {
+    s = src + q; d = dst + q; w = 1;
+  }
+}
+__device__ __forceinline__ uint4 load_w(const uint8_t* s, uint32_t w) {
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (w == 16) __builtin_memcpy(&v, s, 16);
+  else if (w == 8) __builtin_memcpy(&v, s, 8);
+  else if (w == 4) __builtin_memcpy(&v, s, 4);
+  else v.x = *s;
+  return v;
+}
+__device__ __forceinline__ void store_w(uint8_t* d, uint4 v, uint32_t w) {
+  if (w == 16) __builtin_memcpy(d, &v, 16);
+  else if (w == 8) __builtin_memcpy(d, &v, 8);
+  else if (w == 4) __builtin_memcpy(d, &v, 4);
+  else *d = (uint8_t)v.x;
+}
+template <uint32_t J, uint32_t G, class Rec>
+__device__ __forceinline__ void copy_bytes_batched(const Rec& rec, const uint8_t* blk, uint8_t* kbase,
+                                                   uint8_t* vbase, uint32_t n, uint32_t lane) {
+  const uint32_t j = lane & (J - 1);
+  for (uint32_t e0 = 0; e0 < n; e0 += G * (kWave / J)) {
+    uint32_t hp[G], kl[G], vl[G], ko[G], vo[G], np[G], kp[G];
+    bool on[G];
+#pragma unroll
+    for (int i = 0; i < (int)G; i++) {
+      const uint32_t e = e0 + i * (kWave / J) + lane / J;
+      const uint32_t ec = min(e, n - 1);
+      const uint32_t m0 = rec(ec), m1 = rec(ec + 1);
+      hp[i] = m0 & 0xffffu;
+      vo[i] = m0 >> 16;
+      vl[i] = (m1 >> 16) - vo[i];
+      kl[i] = (m1 & 0xffffu) - hp[i] - 10 - vl[i];
+      ko[i] = hp[i] - 10 * ec - vo[i];
+      on[i] = e < n;
+      kp[i] = pieces16(kl[i]);
+      np[i] = kp[i] + pieces16(vl[i]);
+    }
+    uint4 v[G];
+    uint8_t* d[G];
+    uint32_t w[G];
+#pragma unroll
+    for (int i = 0; i < (int)G; i++) {  // piece j of every entry: all loads first
+      const uint8_t* sp = blk;
+      d[i] = nullptr;
+      w[i] = 0;
+      if (on[i] && j < np[i]) {
+        const bool key = j < kp[i];
+        uint8_t* dst = key ? kbase : vbase;
+        if (dst) {
+          piece_at(blk + (key ? hp[i] + 10 : hp[i] + 10 + kl[i]), dst + (key ? ko[i] : vo[i]),
+                   key ? kl[i] : vl[i], key ? j : j - kp[i], sp, d[i], w[i]);
+          v[i] = load_w(sp, w[i]);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < (int)G; i++)
+      if (d[i]) store_w(d[i], v[i], w[i]);
+#pragma unroll
+    for (int i = 0; i < (int)G; i++) {  // pieces j + J, j + 2J, ... (entries wider than J pieces)
+      if (!on[i]) continue;
+      for (uint32_t q = j + J; q < np[i]; q += J) {
+        const bool key = q < kp[i];
+        uint8_t* dst = key ? kbase : vbase;
+        if (!dst) continue;
+        const uint32_t len = key ? kl[i] : vl[i];
+        const uint32_t s0 = key ? hp[i] + 10 : hp[i] + 10 + kl[i];
+        copy_piece16(dst + (key ? ko[i] : vo[i]), blk + s0, len, key ? q : q - kp[i]);
+      }
+    }
+  }
+}
+
 // a block with prefix-compressed entries (plen > 0: never written by Builder; the
 // format the iterator accepts): entries 64 at a time, lane = entry, plen read from the header,
 // key offsets by a wave scan of plen + stored key bytes; keys bytewise as baseKey[:plen] ++ diff
@@ -181,7 +271,7 @@ __global__ void __launch_bounds__(64) onepass_kernel(DecodeParams p) {
     uint32_t* row = recs + g * R;
     uint32_t* ovf = p.wmeta + (uint64_t)(valid ? b : 0) * p.wcap;
     uint32_t pos = 0, gn = 0, gK = 0, gV = 0, gst = valid && !inrange ? LSMGPU_BLK_RANGE : LSMGPU_BLK_OK;
-    if (inrange && len) {
+    if (p.wprefetch && inrange && len) {
       // one byte of every 128-B line of the block (the first at the block's first byte): the
       // L2 fetches whole lines; independent loads, one wait
       const uintptr_t a0 = (uintptr_t)blk, first = a0 & ~(uintptr_t)127;
@@ -323,10 +413,16 @@ __global__ void __launch_bounds__(64) onepass_kernel(DecodeParams p) {
       entry_outputs(p, rec, nb, enb, ekb, evb, offb, mat, view, lane);
       if (!mat) continue;
       const uint32_t Kb = __builtin_amdgcn_readlane(K, s), Vb = __builtin_amdgcn_readlane(V, s);
-      if ((Kb + Vb) / nb > 128)
+      if (p.wbatch) {
+        if ((Kb + Vb) / nb > 128)
+          copy_bytes_batched<16, 4>(rec, bp, kbase, vbase, nb, lane);
+        else
+          copy_bytes_batched<8, 8>(rec, bp, kbase, vbase, nb, lane);
+      } else if ((Kb + Vb) / nb > 128) {
         copy_bytes<16, 2>(rec, bp, kbase, vbase, nb, lane);
-      else
+      } else {
         copy_bytes<8, 5>(rec, bp, kbase, vbase, nb, lane);
+      }
     }
     wave_lds_fence();  // the next tile's walk overwrites the records
   }

@@ -63,7 +63,6 @@ __device__ __forceinline__ void read_hdr_nt(const uint8_t* g, uint32_t& plen, ui
 // records).  The walk stages 32 records per block in LDS and writes each chunk as one full
 // 128-B line -- 8-B stores straight from 64 lanes at 64 different blocks were evicted from L2 as
 // partial lines (4x the bytes).  Round 3: 4-B records instead of {pos | V << 16, K} (8 B).
-constexpr uint32_t kWalkStage = 33;
 // p.wstatus[b] = the block's status | kPlenFlag when it holds prefix-compressed entries (the
 // walk's K exceeds the stored key bytes, stop pos - 10 n - V): the copy's header-reading path
 constexpr uint32_t kPlenFlag = 1u << 16;  // u32 per lane row: 32 records + 1 pad (bank spread)
@@ -89,10 +88,14 @@ __device__ __forceinline__ void flush_meta(uint32_t* dst, const uint32_t* row, u
 // MODE kWalkLane: lane b walks block b straight from HBM, one dependent 8-B non-temporal header
 // load per entry (every 128-B line of the input is fetched on its own, as scattered requests);
 // the records leave in whole 128-B lines written by 8 lanes each.
-template <int MODE, uint32_t TB>  // TB = blocks per tile (<= 256 threads: thread t owns block t)
+// CH (lane walk): records per flushed chunk -- 32 (whole 128-B lines) or 16 (64-B halves: half
+// the LDS, twice the workgroups per CU)
+template <int MODE, uint32_t TB, uint32_t CH = 32>  // TB = blocks per tile (<= 256 threads)
 __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   static_assert(TB <= 256, "one thread per block of the tile");
-  constexpr uint32_t kStageBytes = 256 * kWalkStage * sizeof(uint32_t);
+  static_assert(CH == 16 || CH == 32, "16 or 32 records per chunk");
+  constexpr uint32_t kStage = CH + 1;  // LDS row per lane: CH records + 1 pad (bank spread)
+  constexpr uint32_t kStageBytes = 256 * kStage * sizeof(uint32_t);
   // group walk: a 32-record ring per block (the walk's LDS also serves the view epilogue's
   // owner map)
   constexpr uint32_t kLdsBytes = MODE == kWalkGroup ? TB * 32 * sizeof(uint32_t) : kStageBytes;
@@ -250,7 +253,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     // 8 lanes per line -- 8 lines per store instruction instead of 64 partial ones (C2 1 GiB,
     // same box: walk 0.233 -> 0.222 ms, view decode 0.271 -> 0.261 ms).
     const bool valid = b < p.nblk;
-    uint32_t* row = stage + tid * kWalkStage;
+    uint32_t* row = stage + tid * kStage;
     uint32_t off = 0, len = 0, pos = 0;
     if (valid) {
       off = p.blk_off[b];
@@ -278,7 +281,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
           if (10 + plen > len) { st = LSMGPU_BLK_PREFIX_OOB; done = true; break; }
           const uint32_t end = pos + 10 + klen + vlen;             // iterator.go:101-109
           if (end > len) { st = LSMGPU_BLK_VALUE_OVERFLOW; done = true; break; }
-          row[n & 31] = pos | (V << 16);
+          row[n & (CH - 1)] = pos | (V << 16);
           K += plen + klen;
           V += vlen;
           n++;
@@ -286,16 +289,17 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
           rec = true;
         } while (false);
       }
-      if ((k & 31) == 31) {
-        const uint64_t fl = __ballot(rec);  // lanes holding records k-31 .. k
+      if ((k & (CH - 1)) == CH - 1) {
+        const uint64_t fl = __ballot(rec);  // lanes holding records k-CH+1 .. k
         if (fl) {
           wave_lds_fence();
+          constexpr uint32_t kPer = CH / 4;  // lanes per row: one 16-B part each
 #pragma unroll
-          for (uint32_t r = 0; r < 8; r++) {
-            const uint32_t L = 8 * r + (lane >> 3), part = lane & 7;
+          for (uint32_t r = 0; r < kPer; r++) {
+            const uint32_t L = (64 / kPer) * r + lane / kPer, part = lane % kPer;
             if ((fl >> L) & 1ull) {
-              const uint32_t* rw = stage + (wave * 64 + L) * kWalkStage + 4 * part;
-              uint32_t* mL = p.wmeta + (uint64_t)(wb0 + L) * p.wcap + (k - 31);
+              const uint32_t* rw = stage + (wave * 64 + L) * kStage + 4 * part;
+              uint32_t* mL = p.wmeta + (uint64_t)(wb0 + L) * p.wcap + (k - (CH - 1));
               reinterpret_cast<uint4*>(mL)[part] = make_uint4(rw[0], rw[1], rw[2], rw[3]);
             }
           }
@@ -306,16 +310,17 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     // the last chunk (records n & ~31 .. n, the sentinel last) of every block, cooperatively as
     // well: whole 128-B lines (the slot holds wcap records, a multiple of 32; words past the
     // sentinel are never read)
-    if (valid) row[n & 31] = pos | (V << 16);
+    if (valid) row[n & (CH - 1)] = pos | (V << 16);
     const uint64_t vm = __ballot(valid);
     wave_lds_fence();
+    constexpr uint32_t kPer = CH / 4;
 #pragma unroll
-    for (uint32_t r = 0; r < 8; r++) {
-      const uint32_t L = 8 * r + (lane >> 3), part = lane & 7;
+    for (uint32_t r = 0; r < kPer; r++) {
+      const uint32_t L = (64 / kPer) * r + lane / kPer, part = lane % kPer;
       const uint32_t nL = (uint32_t)__shfl((int)n, (int)L);
       if ((vm >> L) & 1ull) {
-        const uint32_t* rw = stage + (wave * 64 + L) * kWalkStage + 4 * part;
-        uint32_t* mL = p.wmeta + (uint64_t)(wb0 + L) * p.wcap + (nL & ~31u);
+        const uint32_t* rw = stage + (wave * 64 + L) * kStage + 4 * part;
+        uint32_t* mL = p.wmeta + (uint64_t)(wb0 + L) * p.wcap + (nL & ~(CH - 1));
         reinterpret_cast<uint4*>(mL)[part] = make_uint4(rw[0], rw[1], rw[2], rw[3]);
       }
     }
@@ -663,6 +668,8 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 16>), dim3((nblk + 15) / 16), dim3(256), 0, s, p);
   else if (p.wwalk == kWalkGroup)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 32>), dim3((nblk + 31) / 32), dim3(256), 0, s, p);
+  else if (p.wchunk == 16)
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 256, 16>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
   else
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 256>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
   hipError_t e = hipGetLastError();

@@ -49,6 +49,9 @@ struct DecodeParams {
   uint32_t wwalk;           // walk-scan-copy walk: kWalkLane / kWalkGroup (+ wlanes)
   uint32_t wlanes;          // kWalkGroup: lanes per block (4, 8 or 16)
   uint32_t zero_result;     // walk-scan-copy with a copy launch: the walk zeroes result[0..7]
+  uint32_t wchunk;          // lane walk: records per flushed chunk (16 or 32)
+  uint32_t wprefetch;       // one-pass: fetch each tile's lines before its walk (1) or not (0)
+  uint32_t wbatch;          // one-pass copy: a pass's first pieces loaded before any store (1)
 };
 
 // Encode: one wave per output block; every byte position is closed-form

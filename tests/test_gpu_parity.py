@@ -506,8 +506,8 @@ def test_wsc_lanes_per_entry(codec, oracle, monkeypatch, lanes):
     _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln), f"J={lanes}")
 
 
-@pytest.mark.parametrize("walk", ["lane", "group", "group2", "group4", "group16",
-                                  "one16", "one8", "one4"])
+@pytest.mark.parametrize("walk", ["lane", "lane16", "group", "group2", "group4", "group16",
+                                  "one16", "one8", "one4", "one16b", "one4b"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     """Walk-scan-copy's walks (LSMGPU_WSC_WALK): one lane per block from HBM, or 8 / 4
@@ -516,9 +516,14 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     terminators, plen > 0) at odd alignments, prefix-compressed random blocks, a ragged last
     tile and a block ending at the buffer's end (plus C5 32 KiB blocks for the HBM walks)."""
     from lsmdb_amd.codec import MODE_MATERIALIZE, MODE_VIEW
-    if walk.startswith("one"):  # the one-pass decode, tiles of 16 / 8 / 4 blocks
+    if walk.startswith("one"):  # the one-pass decode, tiles of 16 / 8 / 4 blocks (b: batched)
         monkeypatch.setenv("LSMGPU_DECODE_PATH", "one")
-        monkeypatch.setenv("LSMGPU_ONEPASS_TB", walk[3:])
+        monkeypatch.setenv("LSMGPU_ONEPASS_TB", walk[3:].rstrip("b"))
+        monkeypatch.setenv("LSMGPU_ONEPASS_BATCH", "1" if walk.endswith("b") else "0")
+    elif walk == "lane16":  # the lane walk flushing 16-record (64-B) chunks
+        monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
+        monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
+        monkeypatch.setenv("LSMGPU_WSC_CHUNK", "16")
     else:
         monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
         monkeypatch.setenv("LSMGPU_WSC_WALK", walk)
