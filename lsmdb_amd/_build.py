@@ -8,7 +8,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "lsmdb_amd", "csrc")
 LIB = os.path.join(ROOT, "lsmdb_amd", "liblsmgpu.so")
-SOURCES = ["api.hip", "decode.hip", "decode_wsc.hip", "decode_onepass.hip", "encode.hip", "open_tables.hip", "merge.hip", "bloom.hip", "probe.hip"]
+SOURCES = ["api.hip", "decode.hip", "decode_wsc.hip", "encode.hip", "open_tables.hip", "merge.hip", "bloom.hip", "probe.hip"]
 HEADERS = ["codec_common.hpp", "decode_common.hpp", "kernels.hpp", os.path.join("..", "..", "include", "lsmgpu.h")]
 ARCH = os.environ.get("LSMGPU_ARCH", "gfx950")
 

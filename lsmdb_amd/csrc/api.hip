@@ -340,8 +340,13 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     const char* vf_env = getenv("LSMGPU_WSC_VIEWFUSE");
     const bool fuse = vf_env ? atoi(vf_env) != 0 : nblk >= 512ull * (uint64_t)c->num_cus;
     p.wfuse = !(mode & LSMGPU_MODE_MATERIALIZE) && fuse;
-    const char* ch_env = getenv("LSMGPU_WSC_CHUNK");  // lane walk: 16- or 32-record flushes
+    // lane walk: 32-record (128-B) or 16-record (64-B) flushes.  16 halves the walk's LDS (8
+    // workgroups per CU instead of 4, so C2's 1,041 tiles at 2^30 B are all resident), but
+    // flushes twice as often; same-box A/Bs split (profiles/r04b: walk 0.232 vs 0.226 ms for
+    // 16; profiles/r04d: 0.229 vs 0.236 for 32), so 32 stays the default
+    const char* ch_env = getenv("LSMGPU_WSC_CHUNK");
     p.wchunk = ch_env && atoi(ch_env) == 16 ? 16u : 32u;
+
     const char* wk_env = getenv("LSMGPU_WSC_WALK");
     // Default: 8 lanes per block guessing same-shape runs (kWalkGroup) when the batch has at
     // most 64 blocks per CU -- one lane per block would leave the machine idle and the walk is
@@ -358,25 +363,6 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
       const int l = atoi(wk_env + 5);  // "group" alone: 8 lanes
       p.wwalk = kWalkGroup;
       p.wlanes = l == 2 || l == 4 || l == 16 ? (uint32_t)l : 8u;  // "group2" ... "group16"
-    }
-    // one-pass decode (decode_onepass.hip): LSMGPU_DECODE_PATH=one
-    const char* dp_env = getenv("LSMGPU_DECODE_PATH");
-    const bool onepass_env = dp_env && strncmp(dp_env, "one", 3) == 0;
-    if (onepass_env) {
-      const char* pf_env = getenv("LSMGPU_ONEPASS_PF");  // A/B: 0 = no line fetch before the walk
-      p.wprefetch = pf_env && atoi(pf_env) == 0 ? 0u : 1u;
-      const char* bt_env = getenv("LSMGPU_ONEPASS_BATCH");  // A/B: batched piece loads
-      p.wbatch = bt_env && atoi(bt_env) == 1 ? 1u : 0u;
-      HIPC(hipMemsetAsync(d_result, 0, 8 * sizeof(uint64_t), c->stream));
-      if (c->ktime) HIPC(hipEventRecord(c->kev[0], c->stream));
-      HIPC(launch_decode_onepass(p, max_blk_len, c->num_cus, c->stream));
-      if (c->ktime) {
-        HIPC(hipEventRecord(c->kev[1], c->stream));
-        HIPC(hipEventRecord(c->kev[2], c->stream));
-      }
-      c->kvalid = c->ktime;
-      c->kfused = true;
-      return LSMGPU_OK;
     }
     // d_result is zeroed by the walk kernel when a copy launch follows it (the copy's atomics
     // come after the kernel boundary): one operation fewer per decode.  A view-only decode

@@ -1269,9 +1269,9 @@ static hipError_t launch_cfg(const DecodeParams& p, int num_cus, hipStream_t s,
 }
 
 int decode_path(uint32_t max_blk_len, uint32_t nblk) {
-  // LSMGPU_DECODE_PATH=reg|lds|wsc|one forces a path (A/B diagnostics and tests)
+  // LSMGPU_DECODE_PATH=reg|lds|wsc forces a path (A/B diagnostics and tests)
   const char* f = getenv("LSMGPU_DECODE_PATH");
-  if (f && (f[0] == 'w' || f[0] == 'o') && max_blk_len < 65536) return 2;  // wsc / one-pass
+  if (f && f[0] == 'w' && max_blk_len < 65536) return 2;
   if (f && f[0] == 'l') return 1;
   if (f && f[0] == 'r' && max_blk_len <= 4096) return 0;
   // walk-scan-copy is three launches (walk, scan, copy): it wins from ~1k blocks up; small

@@ -648,6 +648,9 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   // (C2: copy 0.504 -> 0.485 ms; C5 / C3 blocks of fewer, larger entries lose 3 % that way, so
   // their 16-lane groups keep writing them)
   const uint32_t avg = (K + V) / n;
+  // (round 4: each lane's first piece of every entry of a pass loaded before any store left
+  // the copy unchanged, 0.6038 vs 0.6042 ms, profiles/r04c; compiled into this kernel it also
+  // raised the VGPRs from 44 to 90, 8 -> 5 waves per SIMD: removed)
   if (p.wj == 16 || (p.wj == 0 && avg > 128)) {
     copy_entries<16, 2, true>(p, meta, blk, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
   } else {

@@ -50,8 +50,7 @@ struct DecodeParams {
   uint32_t wlanes;          // kWalkGroup: lanes per block (4, 8 or 16)
   uint32_t zero_result;     // walk-scan-copy with a copy launch: the walk zeroes result[0..7]
   uint32_t wchunk;          // lane walk: records per flushed chunk (16 or 32)
-  uint32_t wprefetch;       // one-pass: fetch each tile's lines before its walk (1) or not (0)
-  uint32_t wbatch;          // one-pass copy: a pass's first pieces loaded before any store (1)
+
 };
 
 // Encode: one wave per output block; every byte position is closed-form
@@ -171,11 +170,7 @@ hipError_t launch_encode(const EncodeParams& p, int num_cus, hipStream_t s);
 // the caller; p.gcnt[0] = 0 between launches (the walk's tile ticket), p.lb tile records
 // mid (optional): an event recorded between the walk and the copy launch (kernel timing)
 hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mid = nullptr);
-// one-pass decode (decode_onepass.hip, blocks < 64 KiB): wave workers over ticket-ordered tiles,
-// the input read from HBM once; p.wmeta / p.wcap = the spill for records past the LDS slot,
-// p.gcnt[0] = 0 between launches, p.lb tile records, p.result zeroed before the launch
-hipError_t launch_decode_onepass(const DecodeParams& p, uint32_t max_blk_len, int num_cus,
-                                 hipStream_t s);
+
 // bloom tail (bloom.hip; bbloom restated, table/builder.go:164-195, table/table.go:301)
 struct BloomParams {
   const uint8_t* keys;

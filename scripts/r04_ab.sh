@@ -1,0 +1,47 @@
+#!/bin/bash
+# Round-4 same-box A/B: walk-scan-copy knobs (flush chunk), the E2E host pipeline through the C
+# ABI, and the other configs.  (The one-pass decode's phase stamps of profiles/r04c came from
+# this script's removed "s" part.)
+# Usage (on the GPU box): bash scripts/r04_ab.sh <tag> [parts]   parts: any of t a e c (default all)
+set -o pipefail
+T=${1:-r04ab}
+PARTS=${2:-"t a e c"}
+O=gpurun_out/$T
+mkdir -p $O
+has() { [[ " $PARTS " == *" $1 "* ]]; }
+line() {  # name json: one summary line
+  python - "$2" "$1" <<'EOF'
+import json, sys
+j = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+r = j["roofline"]; k = r.get("kernels") or {}
+print(sys.argv[2], j["value"], "GiB/s", r["kernel_ms_mean"], "ms | walk", k.get("walk_ms"), "copy",
+      k.get("copy_ms"), "| view", (j.get("view_mode") or {}).get("kernel_ms"), "ms",
+      (j.get("view_mode") or {}).get("read_frac"))
+EOF
+}
+run() {  # name config env...
+  local name=$1 cfg=$2; shift 2
+  env "$@" timeout -k 10 200 python bench.py --config $cfg --no-cpu --no-peaks --steps 20 \
+    > $O/bench_$name.json 2> $O/bench_$name.err || { tail -20 $O/bench_$name.err; exit 1; }
+  line $name $O/bench_$name.json
+}
+if has t; then
+  timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread \
+    -k "walk_modes or many_tiles or forced or adversarial or mixed_copy" > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+  tail -1 $O/tests.log
+fi
+if has a; then
+  run c2_ch16 2
+  run c2_ch32 2 LSMGPU_WSC_CHUNK=32
+  run c2_ch16b 2
+  run c2_ch32b 2 LSMGPU_WSC_CHUNK=32
+fi
+if has e; then
+  timeout -k 10 300 python scripts/e2e_abi.py > $O/e2e.json 2> $O/e2e.err || { tail -20 $O/e2e.err; exit 1; }
+  cat $O/e2e.json
+fi
+if has c; then
+  for cfg in 3 4 5; do
+    run c${cfg} $cfg
+  done
+fi

@@ -6,8 +6,10 @@ Reads are counted by request size -- TCC_EA0_RDREQ_{32B,64B,128B} x {32, 64, 128
 access-width calibration is assumed (MI355X_MICROARCH.md: FETCH_SIZE tallies 128-B requests at
 64 B; only wide streaming reads are calibrated).  Writes: TCC_EA0_WRREQ_64B x 64 B + the other
 write requests x 32 B.  FETCH_SIZE x 2 and WRITE_SIZE are kept beside them as a cross-check.
-Infinity-Cache hits are counted, not excluded (guide): at 1 GiB of input the walk's and the
-copy's reads of the same lines cannot both stay in the 256 MiB cache.
+Infinity-Cache hits are counted, not excluded (guide): the TCC_EA0 counters are the L2's requests
+to the fabric, whichever of the Infinity Cache or HBM serves them -- at 1 GiB of input the walk's
+and the copy's reads of the same lines cannot both stay in the 256 MiB cache, and the one-pass
+kernel's walk / copy re-reads that miss L2 are counted though the Infinity Cache serves them.
 
 usage: traffic_summary.py <rd.csv> <wr.csv> <fetch.csv> <write.csv> <bench.json> <out.json>
 """
@@ -18,7 +20,7 @@ import os
 import sys
 
 PIPELINE = ("lsmgpu::decode", "wsc_walk_kernel", "wsc_copy_kernel", "wsc_carry_kernel", "Tri64",
-            "tile_decode_kernel", "fsw_kernel", "fsc_kernel")
+            "tile_decode_kernel", "fsw_kernel", "fsc_kernel", "onepass_kernel")
 
 
 def per_launch(path, counters):

@@ -25,7 +25,7 @@ def _shard(oracle, cfg, n, seed):
     return _sst_blocks(oracle, [sst])
 
 
-@pytest.mark.parametrize("path", [None, "wsc", "one"])
+@pytest.mark.parametrize("path", [None, "wsc"])
 def test_two_contexts_concurrently(oracle, monkeypatch, path):
     if path:
         monkeypatch.setenv("LSMGPU_DECODE_PATH", path)

@@ -323,7 +323,7 @@ def test_many_rounds(codec, oracle, monkeypatch, grid, shape):
     assert g.val_data.tobytes() == cols[2].tobytes()
 
 
-@pytest.mark.parametrize("path", ["wsc", "one", "lds", "reg"])
+@pytest.mark.parametrize("path", ["wsc", "lds", "reg"])
 def test_forced_decode_paths(codec, oracle, monkeypatch, path):
     """Every decode path (LSMGPU_DECODE_PATH: walk-scan-copy, LDS-lag, register-lag) on the
     4 KiB block shapes: C2 4 KiB blocks, short entries, the KAT blocks (every
@@ -405,7 +405,7 @@ def test_wsc_split(codec, oracle, monkeypatch, split):
     test_prefix_compressed_random(codec, oracle)
 
 
-@pytest.mark.parametrize("path", [None, "wsc", "one", "lds"])
+@pytest.mark.parametrize("path", [None, "wsc", "lds"])
 def test_prefix_compressed_large_output(codec, oracle, monkeypatch, path):
     """Prefix-compressed blocks whose OUTPUT keys exceed 64 KiB per block (plen ~ 3000 on
     ~4000-byte... up to 60 KiB blocks of tiny entries): per-entry key offsets must not be held
@@ -449,22 +449,20 @@ def test_prefix_compressed_large_output(codec, oracle, monkeypatch, path):
     _assert_same(codec.decode_host(data, off, ln), ref, f"path={path}")
 
 
-@pytest.mark.parametrize("path,wpc", [(None, None), ("one", "12"), ("one", "1"), ("one", "32")])
-def test_wsc_many_tiles(codec, oracle, monkeypatch, path, wpc):
+@pytest.mark.parametrize("chunk", ["32", "16"])
+def test_wsc_many_tiles(codec, oracle, monkeypatch, chunk):
     """The walk kernel's tiles (256 blocks, ticket order) find their output bases by decoupled
     look-back over ~40 tile records: C2 blocks plus a ragged last tile, checked against the
-    oracle on every output array.  The one-pass decode: ~660 tiles of 16 blocks over 1 / 12 /
-    32 workers per CU (LSMGPU_ONEPASS_WPC), three launches back to back (the ticket reset)."""
-    if path:
-        monkeypatch.setenv("LSMGPU_DECODE_PATH", path)
-        monkeypatch.setenv("LSMGPU_ONEPASS_WPC", wpc)
+    oracle on every output array, three launches back to back (the ticket reset); 32- and
+    16-record flush chunks."""
+    monkeypatch.setenv("LSMGPU_WSC_CHUNK", chunk)
     c = _cols(2, 330000, seed=13)
     sst, _, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, 0, 4096)
     sst = sst + b"{}" + (2).to_bytes(4, "big")
     off, ln, _, _ = oracle.parse_index(sst)
     assert len(off) > 39 * 256 and len(off) % 256 != 0
     ref = oracle.decode(sst, off, ln)
-    for _ in range(3 if path else 1):
+    for _ in range(3):
         g = codec.decode_host(sst, off, ln)
         _assert_same(g, ref, "many tiles")
     assert g.key_data.tobytes() == c.keys.tobytes()
@@ -506,8 +504,7 @@ def test_wsc_lanes_per_entry(codec, oracle, monkeypatch, lanes):
     _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln), f"J={lanes}")
 
 
-@pytest.mark.parametrize("walk", ["lane", "lane16", "group", "group2", "group4", "group16",
-                                  "one16", "one8", "one4", "one16b", "one4b"])
+@pytest.mark.parametrize("walk", ["lane", "lane16", "group", "group2", "group4", "group16"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     """Walk-scan-copy's walks (LSMGPU_WSC_WALK): one lane per block from HBM, or 8 / 4
@@ -516,16 +513,11 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     terminators, plen > 0) at odd alignments, prefix-compressed random blocks, a ragged last
     tile and a block ending at the buffer's end (plus C5 32 KiB blocks for the HBM walks)."""
     from lsmdb_amd.codec import MODE_MATERIALIZE, MODE_VIEW
-    if walk.startswith("one"):  # the one-pass decode, tiles of 16 / 8 / 4 blocks (b: batched)
-        monkeypatch.setenv("LSMGPU_DECODE_PATH", "one")
-        monkeypatch.setenv("LSMGPU_ONEPASS_TB", walk[3:].rstrip("b"))
-        monkeypatch.setenv("LSMGPU_ONEPASS_BATCH", "1" if walk.endswith("b") else "0")
-    elif walk == "lane16":  # the lane walk flushing 16-record (64-B) chunks
-        monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
+    monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
+    if walk == "lane16":  # the lane walk flushing 16-record (64-B) chunks
         monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
         monkeypatch.setenv("LSMGPU_WSC_CHUNK", "16")
     else:
-        monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
         monkeypatch.setenv("LSMGPU_WSC_WALK", walk)
     monkeypatch.setenv("LSMGPU_WSC_VIEWFUSE", "1")
     c2 = _cols(2, 40000, seed=23)
@@ -612,7 +604,7 @@ def _block_entries(block):
     return out
 
 
-@pytest.mark.parametrize("walk", ["lane", "group", "one"])
+@pytest.mark.parametrize("walk", ["lane", "lane16", "group"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
     """Blocks built to defeat a header-pattern filter, decoded by every walk.  Keys and
@@ -623,8 +615,9 @@ def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
     terminator, a torn terminator, torn entries).  Every block must decode exactly as the
     oracle's iterator does."""
     from lsmdb_amd.codec import MODE_MATERIALIZE, MODE_VIEW
-    monkeypatch.setenv("LSMGPU_DECODE_PATH", "one" if walk == "one" else "wsc")
-    monkeypatch.setenv("LSMGPU_WSC_WALK", "lane" if walk == "one" else walk)
+    monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
+    monkeypatch.setenv("LSMGPU_WSC_WALK", "lane" if walk == "lane16" else walk)
+    monkeypatch.setenv("LSMGPU_WSC_CHUNK", "16" if walk == "lane16" else "32")
     monkeypatch.setenv("LSMGPU_WSC_VIEWFUSE", "1")
     rng = np.random.default_rng(77)
     parts = []

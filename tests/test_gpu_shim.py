@@ -120,7 +120,16 @@ def test_shim_decode_table_pipelined(codec, oracle, monkeypatch):
 def test_shim_decode_expanding_and_bad_blocks(codec, oracle):
     """Prefix-compressed keys that expand past the input's size: the first call returns
     LSMGPU_ERR_CAPACITY with the exact needs (and the bad-block counts), the second succeeds."""
-    blocks = [K.PLEN_BLOCK] * 40 + [kat[1] for kat in K.DECODE_KATS]
+    import struct
+    big = bytearray()  # 4,000 entries of plen 2,900: ~11.6 MB of keys from a 20 KB block
+    prev = 0xFFFFFFFF
+    for e in range(4000):
+        pos = len(big)
+        plen, diff = (0, bytes(range(256)) * 12) if e == 0 else (2900, b"x")
+        big += struct.pack(">HHHI", plen, len(diff), 1, prev) + diff + b"v"
+        prev = pos
+    big += struct.pack(">HHHI", 0, 0, 3, prev) + b"\0\0\0"
+    blocks = [K.PLEN_BLOCK] * 40 + [bytes(big)] + [kat[1] for kat in K.DECODE_KATS]
     data = b"".join(blocks)
     ends = np.cumsum([len(b) for b in blocks]).astype(np.uint32)
     sst = C.with_tail(data, ends)
