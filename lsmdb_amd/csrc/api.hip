@@ -346,6 +346,10 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     // 16; profiles/r04d: 0.229 vs 0.236 for 32), so 32 stays the default
     const char* ch_env = getenv("LSMGPU_WSC_CHUNK");
     p.wchunk = ch_env && atoi(ch_env) == 16 ? 16u : 32u;
+    // view-only lane walk: the records stay in LDS (kWalkLaneView); LSMGPU_WSC_VIEWKEEP=0 flushes
+    // them to p.wmeta and re-reads them in the owner-map epilogue instead (round 3)
+    const char* vk_env = getenv("LSMGPU_WSC_VIEWKEEP");
+    p.wkeep = vk_env && atoi(vk_env) == 0 ? 0u : 1u;
 
     const char* wk_env = getenv("LSMGPU_WSC_WALK");
     // Default: 8 lanes per block guessing same-shape runs (kWalkGroup) when the batch has at

@@ -90,23 +90,29 @@ __device__ __forceinline__ void flush_meta(uint32_t* dst, const uint32_t* row, u
 // the records leave in whole 128-B lines written by 8 lanes each.
 // CH (lane walk): records per flushed chunk -- 32 (whole 128-B lines) or 16 (64-B halves: half
 // the LDS, twice the workgroups per CU)
+// MODE kWalkLaneView (view-only decodes, round 4): the lane walk keeping each block's first
+// kViewRec records in its LDS row for the whole kernel -- no flush during the walk, no re-read:
+// after the look-back each wave writes its 64 blocks' view records from LDS (records past
+// kViewRec, rare, go to / come from p.wmeta)
 template <int MODE, uint32_t TB, uint32_t CH = 32>  // TB = blocks per tile (<= 256 threads)
 __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   static_assert(TB <= 256, "one thread per block of the tile");
   static_assert(CH == 16 || CH == 32, "16 or 32 records per chunk");
-  constexpr uint32_t kStage = CH + 1;  // LDS row per lane: CH records + 1 pad (bank spread)
+  constexpr bool KEEP = MODE == kWalkLaneView;
+  // LDS row per lane: CH records (+ 1 pad, bank spread), or kViewRec kept records (+ 1)
+  constexpr uint32_t kStage = KEEP ? kViewRec + 1 : CH + 1;
   constexpr uint32_t kStageBytes = 256 * kStage * sizeof(uint32_t);
   // group walk: a 32-record ring per block (the walk's LDS also serves the view epilogue's
   // owner map)
   constexpr uint32_t kLdsBytes = MODE == kWalkGroup ? TB * 32 * sizeof(uint32_t) : kStageBytes;
-  static_assert(MODE != kWalkLane || kLdsBytes == kStageBytes,
-                "the lane walk stages 32 records per lane");
+  static_assert(MODE == kWalkGroup || kLdsBytes == kStageBytes,
+                "the lane walk stages its records per lane");
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   uint32_t* const stage = reinterpret_cast<uint32_t*>(lds);
   __shared__ uint32_t s_tile;
   __shared__ uint32_t s_wave[4][3];
   __shared__ uint32_t s_ex[3];
-  __shared__ uint32_t s_first[257];  // p.wfuse: tile-relative first entry of each block
+  __shared__ uint32_t s_first[KEEP ? 1 : 257];  // p.wfuse: tile-relative first entry of each block
   __shared__ uint32_t s_off[MODE == kWalkGroup ? TB : 256];  // each block's input offset
   constexpr uint32_t kRes = MODE == kWalkGroup ? TB : 1;
   __shared__ uint32_t s_res[4][kRes];  // group / wave walk: n, K, V, status per block
@@ -281,7 +287,12 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
           if (10 + plen > len) { st = LSMGPU_BLK_PREFIX_OOB; done = true; break; }
           const uint32_t end = pos + 10 + klen + vlen;             // iterator.go:101-109
           if (end > len) { st = LSMGPU_BLK_VALUE_OVERFLOW; done = true; break; }
-          row[n & (CH - 1)] = pos | (V << 16);
+          if constexpr (KEEP) {
+            if (n < kViewRec) row[n] = pos | (V << 16);
+            else p.wmeta[(uint64_t)b * p.wcap + n] = pos | (V << 16);
+          } else {
+            row[n & (CH - 1)] = pos | (V << 16);
+          }
           K += plen + klen;
           V += vlen;
           n++;
@@ -289,7 +300,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
           rec = true;
         } while (false);
       }
-      if ((k & (CH - 1)) == CH - 1) {
+      if (!KEEP && (k & (CH - 1)) == CH - 1) {
         const uint64_t fl = __ballot(rec);  // lanes holding records k-CH+1 .. k
         if (fl) {
           wave_lds_fence();
@@ -310,12 +321,18 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     // the last chunk (records n & ~31 .. n, the sentinel last) of every block, cooperatively as
     // well: whole 128-B lines (the slot holds wcap records, a multiple of 32; words past the
     // sentinel are never read)
-    if (valid) row[n & (CH - 1)] = pos | (V << 16);
-    const uint64_t vm = __ballot(valid);
-    wave_lds_fence();
+    if constexpr (KEEP) {  // the sentinel; the rows stay in LDS
+      if (valid) {
+        if (n < kViewRec) row[n] = pos | (V << 16);
+        else p.wmeta[(uint64_t)b * p.wcap + n] = pos | (V << 16);
+      }
+    }
+    if (valid && !KEEP) row[n & (CH - 1)] = pos | (V << 16);
+    const uint64_t vm = KEEP ? 0ull : __ballot(valid);
+    if (!KEEP) wave_lds_fence();
     constexpr uint32_t kPer = CH / 4;
 #pragma unroll
-    for (uint32_t r = 0; r < kPer; r++) {
+    for (uint32_t r = 0; r < (KEEP ? 0u : kPer); r++) {
       const uint32_t L = (64 / kPer) * r + lane / kPer, part = lane % kPer;
       const uint32_t nL = (uint32_t)__shfl((int)n, (int)L);
       if ((vm >> L) & 1ull) {
@@ -324,7 +341,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
         reinterpret_cast<uint4*>(mL)[part] = make_uint4(rw[0], rw[1], rw[2], rw[3]);
       }
     }
-    if (valid) {
+    if (valid && !KEEP) {  // for the copy kernel (a view-only decode has none)
       uint64_t* t = p.wstat + 3ull * b;
       t[0] = n;
       t[1] = K;
@@ -362,6 +379,8 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     }
   }
   __syncthreads();
+  uint32_t en_b = 0;  // this thread's block's first entry (kWalkLaneView's view loop)
+  const uint32_t off_b = (MODE != kWalkGroup && b < p.nblk) ? s_off[tid] : 0u;
   if (b < p.nblk) {
     uint32_t on = s_ex[0], ok = s_ex[1], ov = s_ex[2];
     for (uint32_t w = 0; w < wave; w++) {
@@ -371,6 +390,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     }
     const uint32_t en = sat_add(on, in_ - n), ek = sat_add(ok, ik == 0xffffffffu ? ik : ik - K),
                    ev = sat_add(ov, iv - V);
+    en_b = en;
     if (!p.wfuse) {
       uint64_t* bs = p.wbase + 3ull * b;
       bs[0] = en;
@@ -395,6 +415,44 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     }
   }
   if (!p.wfuse) return;
+  if constexpr (KEEP) {
+    if (!((p.mode & LSMGPU_MODE_VIEW) && p.view) || (p.ablate & 2)) return;  // mode 0: no view
+    // each wave writes its 64 blocks' records -- consecutive in the output -- one lane per
+    // entry, 64 consecutive 8-B records per store instruction, from the rows its lanes filled:
+    // flat entry f of the wave belongs to the last block L whose wave-exclusive first entry
+    // (pw, lane L) is <= f (6 lane-shuffle steps)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // rows (and any spill) written
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t wb0 = tile * 256 + wave * 64;
+    const uint32_t pw = in_ - n;  // wave-exclusive first entry of this lane's block
+    const uint32_t T = __builtin_amdgcn_readlane(in_, 63);  // the wave's entries (no saturation:
+                                                           // <= 64 x 6,554)
+    const uint64_t ew = __builtin_amdgcn_readlane(en_b, 0);  // the wave's first output entry
+    for (uint32_t c0 = 0; c0 < T; c0 += 64) {
+      const uint32_t f = c0 + lane;
+      uint32_t L = 0;
+#pragma unroll
+      for (uint32_t st = 32; st >= 1; st >>= 1) {
+        const uint32_t cand = L + st;
+        const uint32_t pc = (uint32_t)__shfl((int)pw, (int)min(cand, 63u));
+        if (cand < 64 && pc <= f) L = cand;
+      }
+      const uint32_t pL = (uint32_t)__shfl((int)pw, (int)L), nL = (uint32_t)__shfl((int)n, (int)L);
+      const uint32_t offL = (uint32_t)__shfl((int)off_b, (int)L);
+      if (f >= T) continue;
+      const uint64_t bend = ew + pL + nL;
+      if (!(bend <= p.ent_cap && bend <= 0xffffffffull)) continue;  // reported (result[5])
+      const uint32_t e = f - pL;
+      const uint32_t* rw = stage + (wave * 64 + L) * kStage;
+      const uint32_t* gl = p.wmeta + (uint64_t)(wb0 + L) * p.wcap;
+      const uint32_t m0 = e < kViewRec ? rw[e] : gl[e];
+      const uint32_t m1 = e + 1 < kViewRec ? rw[e + 1] : gl[e + 1];
+      const uint32_t hp = m0 & 0xffffu, vl = (m1 >> 16) - (m0 >> 16);
+      const uint32_t kl = (m1 & 0xffffu) - hp - 10 - vl;  // stored key bytes
+      p.view[ew + f] = (uint64_t)(offL + hp + 10) | ((uint64_t)kl << 32) | ((uint64_t)vl << 48);
+    }
+    return;
+  }
   // View-only decode (p.wfuse): the workgroup writes its tile's dense view records itself, so
   // no copy launch follows.  Output entry e of the tile belongs to the last block whose first
   // entry is <= e (binary search over s_first); its record comes from the walk metadata this
@@ -671,6 +729,8 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 16>), dim3((nblk + 15) / 16), dim3(256), 0, s, p);
   else if (p.wwalk == kWalkGroup)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 32>), dim3((nblk + 31) / 32), dim3(256), 0, s, p);
+  else if (p.wfuse && p.wkeep)
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkLaneView, 256>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
   else if (p.wchunk == 16)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 256, 16>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
   else

@@ -27,14 +27,15 @@ run() {  # name config env...
 }
 if has t; then
   timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread \
-    -k "walk_modes or many_tiles or forced or adversarial or mixed_copy" > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+    -k "walk_modes or many_tiles or forced or adversarial or mixed_copy or view_only" > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
   tail -1 $O/tests.log
 fi
 if has a; then
-  run c2_ch16 2
-  run c2_ch32 2 LSMGPU_WSC_CHUNK=32
-  run c2_ch16b 2
-  run c2_ch32b 2 LSMGPU_WSC_CHUNK=32
+  run c2 2
+  run c2_nokeep 2 LSMGPU_WSC_VIEWKEEP=0
+  run c2_ch16 2 LSMGPU_WSC_CHUNK=16
+  run c2b 2
+  run c2_nokeepb 2 LSMGPU_WSC_VIEWKEEP=0
 fi
 if has e; then
   timeout -k 10 300 python scripts/e2e_abi.py > $O/e2e.json 2> $O/e2e.err || { tail -20 $O/e2e.err; exit 1; }

@@ -504,7 +504,8 @@ def test_wsc_lanes_per_entry(codec, oracle, monkeypatch, lanes):
     _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln), f"J={lanes}")
 
 
-@pytest.mark.parametrize("walk", ["lane", "lane16", "group", "group2", "group4", "group16"])
+@pytest.mark.parametrize("walk", ["lane", "lane16", "lane_flush", "group", "group2", "group4",
+                                  "group16"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     """Walk-scan-copy's walks (LSMGPU_WSC_WALK): one lane per block from HBM, or 8 / 4
@@ -517,6 +518,9 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     if walk == "lane16":  # the lane walk flushing 16-record (64-B) chunks
         monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
         monkeypatch.setenv("LSMGPU_WSC_CHUNK", "16")
+    elif walk == "lane_flush":  # view-only: records flushed and re-read (no LDS-kept rows)
+        monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
+        monkeypatch.setenv("LSMGPU_WSC_VIEWKEEP", "0")
     else:
         monkeypatch.setenv("LSMGPU_WSC_WALK", walk)
     monkeypatch.setenv("LSMGPU_WSC_VIEWFUSE", "1")
