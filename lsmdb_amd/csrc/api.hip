@@ -350,6 +350,8 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     // them to p.wmeta and re-reads them in the owner-map epilogue instead (round 3)
     const char* vk_env = getenv("LSMGPU_WSC_VIEWKEEP");
     p.wkeep = vk_env && atoi(vk_env) == 0 ? 0u : 1u;
+    const char* wt_env = getenv("LSMGPU_WSC_TILE");  // A/B: lane-walk workgroup of 192 / 256
+    p.wtile = wt_env && atoi(wt_env) == 192 ? 192u : 256u;
 
     const char* wk_env = getenv("LSMGPU_WSC_WALK");
     // Default: 8 lanes per block guessing same-shape runs (kWalkGroup) when the batch has at

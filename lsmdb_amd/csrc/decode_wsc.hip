@@ -99,9 +99,13 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   static_assert(TB <= 256, "one thread per block of the tile");
   static_assert(CH == 16 || CH == 32, "16 or 32 records per chunk");
   constexpr bool KEEP = MODE == kWalkLaneView;
+  // lane walks: one thread per block, TB = 192 or 256 threads; the group walk: 256 threads
+  constexpr uint32_t kThreads = MODE == kWalkGroup ? 256 : TB;
+  constexpr uint32_t kWaves = kThreads / 64;
+  static_assert(kThreads % 64 == 0, "whole waves");
   // LDS row per lane: CH records (+ 1 pad, bank spread), or kViewRec kept records (+ 1)
   constexpr uint32_t kStage = KEEP ? kViewRec + 1 : CH + 1;
-  constexpr uint32_t kStageBytes = 256 * kStage * sizeof(uint32_t);
+  constexpr uint32_t kStageBytes = kThreads * kStage * sizeof(uint32_t);
   // group walk: a 32-record ring per block (the walk's LDS also serves the view epilogue's
   // owner map)
   constexpr uint32_t kLdsBytes = MODE == kWalkGroup ? TB * 32 * sizeof(uint32_t) : kStageBytes;
@@ -110,10 +114,10 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   uint32_t* const stage = reinterpret_cast<uint32_t*>(lds);
   __shared__ uint32_t s_tile;
-  __shared__ uint32_t s_wave[4][3];
+  __shared__ uint32_t s_wave[kWaves][3];
   __shared__ uint32_t s_ex[3];
-  __shared__ uint32_t s_first[KEEP ? 1 : 257];  // p.wfuse: tile-relative first entry of each block
-  __shared__ uint32_t s_off[MODE == kWalkGroup ? TB : 256];  // each block's input offset
+  __shared__ uint32_t s_first[KEEP ? 1 : kThreads + 1];  // p.wfuse: tile-relative first entry
+  __shared__ uint32_t s_off[MODE == kWalkGroup ? TB : kThreads];  // each block's input offset
   constexpr uint32_t kRes = MODE == kWalkGroup ? TB : 1;
   __shared__ uint32_t s_res[4][kRes];  // group / wave walk: n, K, V, status per block
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
@@ -272,7 +276,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
       done = true;
     }
     const uint8_t* blk = p.data + off;
-    const uint32_t wb0 = tile * 256 + wave * 64;  // the block of this wave's lane 0
+    const uint32_t wb0 = tile * TB + wave * 64;  // the block of this wave's lane 0
     for (uint32_t k = 0;; k++) {
       if (__ballot(!done) == 0) break;
       bool rec = false;
@@ -360,7 +364,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   __syncthreads();
   if (wave == 0) {
     uint32_t tn = 0, tk = 0, tv = 0;
-    for (int w = 0; w < 4; w++) {
+    for (uint32_t w = 0; w < kWaves; w++) {
       tn = sat_add(tn, s_wave[w][0]);
       tk = sat_add(tk, s_wave[w][1]);
       tv = sat_add(tv, s_wave[w][2]);
@@ -423,7 +427,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     // (pw, lane L) is <= f (6 lane-shuffle steps)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // rows (and any spill) written
     __builtin_amdgcn_wave_barrier();
-    const uint32_t wb0 = tile * 256 + wave * 64;
+    const uint32_t wb0 = tile * TB + wave * 64;
     const uint32_t pw = in_ - n;  // wave-exclusive first entry of this lane's block
     const uint32_t T = __builtin_amdgcn_readlane(in_, 63);  // the wave's entries (no saturation:
                                                            // <= 64 x 6,554)
@@ -461,11 +465,11 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     uint32_t rel = in_ - n;  // entries of the tile never saturate (<= 256 x 6,554)
     for (uint32_t w = 0; w < wave; w++) rel += s_wave[w][0];
     s_first[tid] = rel;
-    if (tid == 255) s_first[256] = rel + n;
+    if (tid == kThreads - 1) s_first[kThreads] = rel + n;
   }
   __syncthreads();
   if (!((p.mode & LSMGPU_MODE_VIEW) && p.view) || (p.ablate & 2)) return;  // mode 0: no view
-  const uint32_t nt = s_first[256];
+  const uint32_t nt = s_first[kThreads];
   const uint64_t e0 = s_ex[0];
   // entry -> block map in the walk's staging rows (free now): each thread marks its block's
   // entries, so the lookup is one LDS read (tiles of more entries: binary search)
@@ -481,13 +485,13 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   // 4 entries per thread per trip, every record load issued before any view store (the
   // compiler keeps a load behind an earlier store it cannot prove apart)
   constexpr uint32_t kVB = 4;
-  for (uint32_t eb = tid; eb < nt; eb += 256 * kVB) {
+  for (uint32_t eb = tid; eb < nt; eb += kThreads * kVB) {
     uint32_t m0[kVB], m1[kVB], lo[kVB];
     bool on[kVB];
 #pragma unroll
     for (uint32_t u = 0; u < kVB; u++) {
-      const uint32_t e = eb + 256 * u;
-      uint32_t l = 0, hi = 255;
+      const uint32_t e = eb + kThreads * u;
+      uint32_t l = 0, hi = kThreads - 1;
       if (e < nt) {
         if (mapped) {
           l = owner[e];
@@ -511,7 +515,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
       if (!on[u]) continue;
       const uint32_t hp = m0[u] & 0xffffu, vl = (m1[u] >> 16) - (m0[u] >> 16);
       const uint32_t kl = (m1[u] & 0xffffu) - hp - 10 - vl;  // stored key bytes
-      p.view[e0 + eb + 256 * u] =
+      p.view[e0 + eb + kThreads * u] =
           (uint64_t)(s_off[lo[u]] + hp + 10) | ((uint64_t)kl << 32) | ((uint64_t)vl << 48);
     }
   }
@@ -729,10 +733,14 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 16>), dim3((nblk + 15) / 16), dim3(256), 0, s, p);
   else if (p.wwalk == kWalkGroup)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 32>), dim3((nblk + 31) / 32), dim3(256), 0, s, p);
+  else if (p.wfuse && p.wkeep && p.wtile == 192)
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkLaneView, 192>), dim3((nblk + 191) / 192), dim3(192), 0, s, p);
   else if (p.wfuse && p.wkeep)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLaneView, 256>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
   else if (p.wchunk == 16)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 256, 16>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
+  else if (p.wtile == 192)
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 192>), dim3((nblk + 191) / 192), dim3(192), 0, s, p);
   else
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 256>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
   hipError_t e = hipGetLastError();

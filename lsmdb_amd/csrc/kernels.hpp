@@ -51,6 +51,7 @@ struct DecodeParams {
   uint32_t zero_result;     // walk-scan-copy with a copy launch: the walk zeroes result[0..7]
   uint32_t wchunk;          // lane walk: records per flushed chunk (16 or 32)
   uint32_t wkeep;           // view-only lane walk: records kept in LDS (kWalkLaneView)
+  uint32_t wtile;           // lane walks: blocks (= threads) per workgroup, 192 or 256
 
 };
 
@@ -226,7 +227,7 @@ hipError_t launch_bloom_json(const BloomJson& p, hipStream_t s);
 constexpr int kWalkLane = 0;    // one lane per block, header by header from HBM
 constexpr int kWalkGroup = 2;   // wlanes lanes per block, speculative same-shape runs from HBM
 constexpr int kWalkLaneView = 3;  // view-only lane walk keeping each block's records in LDS
-constexpr uint32_t kViewRec = 36;  // records a kWalkLaneView LDS row keeps (more go to wmeta)
+constexpr uint32_t kViewRec = 33;  // records a kWalkLaneView LDS row keeps (more go to wmeta)
 // which decode path a batch takes: 0 register-lag (<= 4 KiB), 1 LDS-lag, 2 walk-scan-copy
 // (blocks < 64 KiB, batches of >= kWscMinBlocks blocks)
 constexpr uint32_t kWscMinBlocks = 1024;

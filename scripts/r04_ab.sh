@@ -32,10 +32,9 @@ if has t; then
 fi
 if has a; then
   run c2 2
-  run c2_nokeep 2 LSMGPU_WSC_VIEWKEEP=0
-  run c2_ch16 2 LSMGPU_WSC_CHUNK=16
+  run c2_t192 2 LSMGPU_WSC_TILE=192
   run c2b 2
-  run c2_nokeepb 2 LSMGPU_WSC_VIEWKEEP=0
+  run c2_t192b 2 LSMGPU_WSC_TILE=192
 fi
 if has e; then
   timeout -k 10 300 python scripts/e2e_abi.py > $O/e2e.json 2> $O/e2e.err || { tail -20 $O/e2e.err; exit 1; }

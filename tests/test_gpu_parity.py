@@ -504,8 +504,8 @@ def test_wsc_lanes_per_entry(codec, oracle, monkeypatch, lanes):
     _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln), f"J={lanes}")
 
 
-@pytest.mark.parametrize("walk", ["lane", "lane16", "lane_flush", "group", "group2", "group4",
-                                  "group16"])
+@pytest.mark.parametrize("walk", ["lane", "lane16", "lane192", "lane_flush", "group", "group2",
+                                  "group4", "group16"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     """Walk-scan-copy's walks (LSMGPU_WSC_WALK): one lane per block from HBM, or 8 / 4
@@ -518,6 +518,9 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     if walk == "lane16":  # the lane walk flushing 16-record (64-B) chunks
         monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
         monkeypatch.setenv("LSMGPU_WSC_CHUNK", "16")
+    elif walk == "lane192":  # lane-walk workgroups of 192 blocks
+        monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
+        monkeypatch.setenv("LSMGPU_WSC_TILE", "192")
     elif walk == "lane_flush":  # view-only: records flushed and re-read (no LDS-kept rows)
         monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
         monkeypatch.setenv("LSMGPU_WSC_VIEWKEEP", "0")
@@ -608,7 +611,7 @@ def _block_entries(block):
     return out
 
 
-@pytest.mark.parametrize("walk", ["lane", "lane16", "group"])
+@pytest.mark.parametrize("walk", ["lane", "lane16", "lane192", "group"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
     """Blocks built to defeat a header-pattern filter, decoded by every walk.  Keys and
@@ -620,8 +623,9 @@ def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
     oracle's iterator does."""
     from lsmdb_amd.codec import MODE_MATERIALIZE, MODE_VIEW
     monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
-    monkeypatch.setenv("LSMGPU_WSC_WALK", "lane" if walk == "lane16" else walk)
+    monkeypatch.setenv("LSMGPU_WSC_WALK", "lane" if walk in ("lane16", "lane192") else walk)
     monkeypatch.setenv("LSMGPU_WSC_CHUNK", "16" if walk == "lane16" else "32")
+    monkeypatch.setenv("LSMGPU_WSC_TILE", "192" if walk == "lane192" else "256")
     monkeypatch.setenv("LSMGPU_WSC_VIEWFUSE", "1")
     rng = np.random.default_rng(77)
     parts = []
