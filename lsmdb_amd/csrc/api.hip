@@ -359,7 +359,8 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     // pure latency (C4 64 MiB, 5,163 blocks: 0.106 -> 0.071 ms) -- else one lane per block
     // (C2 1 GiB: lane 0.733 vs group 0.799 ms; C5 1 GiB, 185 blocks per CU whose shapes
     // rarely repeat: lane 1.02 vs group 1.08 ms with its give-up rule, 1.66 ms without).
-    // LSMGPU_WSC_WALK=lane / group / group2 / group4 / group16 forces a walk.
+    // LSMGPU_WSC_WALK=lane / group / group2 / group4 / group16 / group32 / group64 (staged in LDS)
+    // forces a walk.
     p.wwalk = nblk <= 64ull * (uint64_t)c->num_cus ? kWalkGroup : kWalkLane;
     p.wlanes = p.wwalk == kWalkGroup ? 8 : 1;
     if (wk_env && wk_env[0] == 'l') {
@@ -368,12 +369,18 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     } else if (wk_env && strncmp(wk_env, "group", 5) == 0) {
       const int l = atoi(wk_env + 5);  // "group" alone: 8 lanes
       p.wwalk = kWalkGroup;
-      p.wlanes = l == 2 || l == 4 || l == 16 ? (uint32_t)l : 8u;  // "group2" ... "group16"
+      p.wlanes = l == 2 || l == 4 || l == 16 || l == 32 || l == 64 ? (uint32_t)l : 8u;  // "group2" ... "group64"
     }
+    // the 64-lane staged walk copies its own blocks from LDS (no copy launch, one read of the
+    // input) unless LSMGPU_WSC_STAGECOPY=0
+    const char* sc_env = getenv("LSMGPU_WSC_STAGECOPY");
+    p.wscopy = p.wwalk == kWalkGroup && p.wlanes == 64 && !p.wfuse && !(sc_env && atoi(sc_env) == 0);
+    const char* sl_env = getenv("LSMGPU_WSC_SLOT");  // A/B: "small" LDS slots (4.25 KiB)
+    p.wslot = sl_env && sl_env[0] == 's' ? 1u : 0u;
     // d_result is zeroed by the walk kernel when a copy launch follows it (the copy's atomics
     // come after the kernel boundary): one operation fewer per decode.  A view-only decode
     // that ends in the walk updates d_result from every workgroup, so it is zeroed first.
-    if (p.wfuse) HIPC(hipMemsetAsync(d_result, 0, 8 * sizeof(uint64_t), c->stream));
+    if (p.wfuse || p.wscopy) HIPC(hipMemsetAsync(d_result, 0, 8 * sizeof(uint64_t), c->stream));
     else p.zero_result = 1;
     if (c->ktime) HIPC(hipEventRecord(c->kev[0], c->stream));
     HIPC(launch_decode_wsc(p, c->stream, c->ktime ? c->kev[1] : nullptr));

@@ -51,6 +51,18 @@ __device__ __forceinline__ void read_hdr_nt(const uint8_t* g, uint32_t& plen, ui
   vlen = __builtin_amdgcn_perm(0u, w.y, 0x0c0c0001u);
 }
 
+// the same from a block staged in LDS at byte offset o (any alignment): three aligned dword
+// reads and two byte-aligns
+__device__ __forceinline__ void read_hdr_lds(const uint32_t* d, uint32_t o, uint32_t& plen,
+                                             uint32_t& klen, uint32_t& vlen) {
+  const uint32_t i = o >> 2, sh = o & 3u;
+  const uint32_t w0 = d[i], w1 = d[i + 1], w2 = d[i + 2];
+  const uint32_t x = __builtin_amdgcn_alignbyte(w1, w0, sh), y = __builtin_amdgcn_alignbyte(w2, w1, sh);
+  plen = __builtin_amdgcn_perm(0u, x, 0x0c0c0001u);
+  klen = __builtin_amdgcn_perm(0u, x, 0x0c0c0203u);
+  vlen = __builtin_amdgcn_perm(0u, y, 0x0c0c0001u);
+}
+
 }  // namespace
 
 // Per-entry metadata of the walk: one u32 record {header pos | value offset << 16} per entry
@@ -77,6 +89,45 @@ __device__ __forceinline__ void flush_meta(uint32_t* dst, const uint32_t* row, u
   }
 }
 
+// Where the copy reads a block's bytes: global memory (the copy kernel), or the walk's LDS slot
+// holding the block at byte sh (the 64-lane staged walk copying its own block, p.wscopy).
+// piece(dst, s0, len, q) = copy_piece16(dst, block + s0, len, q).
+struct GlobalBytes {
+  const uint8_t* b;
+  __device__ __forceinline__ void piece(uint8_t* dst, uint32_t s0, uint32_t len, uint32_t q) const {
+    copy_piece16(dst, b + s0, len, q);
+  }
+};
+struct LdsBytes {
+  const uint8_t* l;
+  uint32_t sh;
+  __device__ __forceinline__ void piece(uint8_t* dst, uint32_t s0, uint32_t len, uint32_t q) const {
+    const uint32_t a = sh + s0;
+    if (len >= 16) {
+      const uint32_t o = min(16 * q, len - 16);
+      const uint4 v = lds_u128(l, a + o);
+      __builtin_memcpy(dst + o, &v, 16);
+    } else if (len >= 8) {
+      const uint32_t o = q ? len - 8 : 0;
+      const uint2 v = make_uint2(lds_u32(l, a + o), lds_u32(l, a + o + 4));
+      __builtin_memcpy(dst + o, &v, 8);
+    } else if (len >= 4) {
+      const uint32_t o = q ? len - 4 : 0;
+      const uint32_t v = lds_u32(l, a + o);
+      __builtin_memcpy(dst + o, &v, 4);
+    } else {
+      dst[q] = l[a + q];
+    }
+  }
+};
+
+template <typename Src>
+__device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, const uint32_t* meta,
+                                           uint32_t pre, uint32_t n, uint32_t K, uint32_t V,
+                                           uint32_t sw, uint64_t en, uint64_t ek, uint64_t ev,
+                                           uint32_t off, uint32_t sub, uint32_t split,
+                                           uint32_t lane, const Src& src);
+
 // K1: lane = block; a workgroup = a tile of 256 consecutive blocks, tiles taken in ticket order
 // (p.gcnt[0]).  After the walk the workgroup scans its blocks' {entries, key bytes, value
 // bytes}, publishes the tile aggregate and finds the tile's output base by decoupled look-back
@@ -94,7 +145,8 @@ __device__ __forceinline__ void flush_meta(uint32_t* dst, const uint32_t* row, u
 // kViewRec records in its LDS row for the whole kernel -- no flush during the walk, no re-read:
 // after the look-back each wave writes its 64 blocks' view records from LDS (records past
 // kViewRec, rare, go to / come from p.wmeta)
-template <int MODE, uint32_t TB, uint32_t CH = 32>  // TB = blocks per tile (<= 256 threads)
+// SLOT: the staged walk's LDS bytes per block
+template <int MODE, uint32_t TB, uint32_t CH = 32, uint32_t SLOT = kStageSlot>  // TB = blocks per tile
 __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   static_assert(TB <= 256, "one thread per block of the tile");
   static_assert(CH == 16 || CH == 32, "16 or 32 records per chunk");
@@ -108,7 +160,14 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   constexpr uint32_t kStageBytes = kThreads * kStage * sizeof(uint32_t);
   // group walk: a 32-record ring per block (the walk's LDS also serves the view epilogue's
   // owner map)
-  constexpr uint32_t kLdsBytes = MODE == kWalkGroup ? TB * 32 * sizeof(uint32_t) : kStageBytes;
+  // group walk of 64 lanes (TB = 4, one wave per block): the wave first copies its block into an
+  // LDS slot with every load in flight, then walks it there (kStaged; blocks too long for a
+  // slot walk from global memory)
+  constexpr bool kStaged = MODE == kWalkGroup && TB == 4;
+  constexpr uint32_t kSlot = kStaged ? SLOT : 0u;
+  static_assert(SLOT % 16 == 0, "16-B chunks");
+  constexpr uint32_t kLdsBytes =
+      MODE == kWalkGroup ? TB * 32 * sizeof(uint32_t) + TB * kSlot : kStageBytes;
   static_assert(MODE == kWalkGroup || kLdsBytes == kStageBytes,
                 "the lane walk stages its records per lane");
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
@@ -120,6 +179,10 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   __shared__ uint32_t s_off[MODE == kWalkGroup ? TB : kThreads];  // each block's input offset
   constexpr uint32_t kRes = MODE == kWalkGroup ? TB : 1;
   __shared__ uint32_t s_res[4][kRes];  // group / wave walk: n, K, V, status per block
+  __shared__ uint32_t s_stg[kStaged ? TB : 1];  // the block is in its LDS slot
+  __shared__ uint32_t s_cb[3][kStaged ? TB : 1];  // p.wscopy: each block's output bases
+  // the staged walk copying its own blocks (p.wscopy): no records for a copy launch
+  const bool scopy = kStaged && p.wscopy && !p.wfuse;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t ntiles = (p.nblk + TB - 1) / TB;
   if (tid == 0) {
@@ -144,8 +207,8 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     // guessed lines belong to the next entries of the same block (no extra traffic), the group
     // fetches neighbouring lines together, and the dependent chain shrinks by the run length.
     constexpr uint32_t L = 256 / TB;
-    static_assert(L >= 2 && L <= 16 && (L & (L - 1)) == 0, "2..16 lanes per block");
-    constexpr uint32_t kMask = (1u << L) - 1;
+    static_assert(L >= 2 && L <= 64 && (L & (L - 1)) == 0, "2..64 lanes per block");
+    constexpr uint64_t kMask = L == 64 ? ~0ull : (1ull << (L & 63)) - 1;
     constexpr uint32_t kGroupProbe = 16;
     const uint32_t g = tid / L, k = tid & (L - 1), gb = lane & ~(L - 1);
     const uint32_t bg = tile * TB + g;
@@ -154,28 +217,70 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
       const uint32_t off = p.blk_off[bg], len = p.blk_len[bg];
       uint32_t* meta = p.wmeta + (uint64_t)bg * p.wcap;
       uint32_t pos = 0, gn = 0, gK = 0, gV = 0, gst = LSMGPU_BLK_OK;
+      bool staged = false;
       if ((uint64_t)off + len > p.data_len) {
         gst = LSMGPU_BLK_RANGE;
       } else {
         const uint8_t* blk = p.data + off;
+        // kStaged: the block's bytes [off & ~15, off + len) as 16-B chunks in the wave's slot,
+        // header q at byte sh + q (chunks past the end of the input load byte by byte)
+        const uint32_t sh = off & 15u;
+        staged = kStaged && sh + len + 16 <= kSlot;
+        const uint32_t* sd = reinterpret_cast<const uint32_t*>(lds + TB * 32 * sizeof(uint32_t) + g * kSlot);
+        if constexpr (kStaged) {
+          if (staged) {
+            const uint64_t a0 = (uint64_t)off - sh;
+            const uint32_t n16 = (sh + len + 15) >> 4;
+            const uint4* src = reinterpret_cast<const uint4*>(p.data + a0);
+            uint4* dst = reinterpret_cast<uint4*>(lds + TB * 32 * sizeof(uint32_t) + g * kSlot);
+            for (uint32_t c0 = 0; c0 < n16; c0 += 8 * L) {
+              uint4 v[8];
+#pragma unroll
+              for (uint32_t u = 0; u < 8; u++) {
+                const uint32_t c = c0 + u * L + k;
+                v[u] = make_uint4(0, 0, 0, 0);
+                if (c < n16) {
+                  if (a0 + 16ull * c + 16 <= p.data_len) {
+                    v[u] = src[c];
+                  } else {  // the input's last partial chunk
+                    uint8_t t[16] = {};
+                    for (uint32_t j = 0; a0 + 16ull * c + j < p.data_len; j++) t[j] = p.data[a0 + 16ull * c + j];
+                    __builtin_memcpy(&v[u], t, 16);
+                  }
+                }
+              }
+#pragma unroll
+              for (uint32_t u = 0; u < 8; u++)
+                if (c0 + u * L + k < n16) dst[c0 + u * L + k] = v[u];
+            }
+            wave_lds_fence();
+          }
+        }
         uint32_t kref = 0xffffffffu, vref = 0, stride = 0;  // no shape yet: round 1 takes one
         uint32_t rounds = 0;
         for (;;) {
-          const uint32_t q = pos + k * stride;  // < 2^21: pos, stride < 2^17, k < 16
+          const uint32_t q = pos + k * stride;  // < 2^24: pos, stride < 2^17, k < 64
           uint32_t plen = 1, klen = 0, vlen = 0;
           // default loads here: the copy after a small batch re-reads the lines from the
           // Infinity Cache (nt guesses: C4 walk 0.038 -> 0.043 ms, copy 0.032 -> 0.042 ms)
-          if (q + 10 <= len) read_hdr(blk + q, plen, klen, vlen);
+          if (q + 10 <= len) {
+            if (staged) read_hdr_lds(sd, sh + q, plen, klen, vlen);
+            else read_hdr(blk + q, plen, klen, vlen);
+          }
           const uint32_t endq = q + 10 + klen + vlen;
           const bool fast = (klen != 0) & (plen == 0) & (endq <= len);
           const bool same = fast & (klen == kref) & (vlen == vref);
-          const uint32_t fb = (uint32_t)(__ballot(fast) >> gb) & kMask;
-          const uint32_t sb = (uint32_t)(__ballot(same) >> gb) & kMask;
+          const uint64_t fb = (__ballot(fast) >> gb) & kMask;
+          const uint64_t sb = (__ballot(same) >> gb) & kMask;
           if (!(fb & 1u)) break;  // entry n itself needs the general loop (or the block ended)
-          const uint32_t t = __builtin_ctz(~sb);                          // leading same-shape run
-          const uint32_t m = t + ((t < L && ((fb >> t) & 1u)) ? 1u : 0u);  // + one new shape
+          uint32_t t = sb == kMask ? L : (uint32_t)__builtin_ctzll(~sb);  // leading same-shape run
+          uint32_t m = t + ((t < L && ((fb >> t) & 1u)) ? 1u : 0u);  // + one new shape
           const uint32_t rec = q | ((gV + k * vref) << 16);
           const uint32_t idx = gn + k, cend = (gn | 31u) + 1;  // end of the current chunk
+          if (L > 32 && gn + m > cend + 32) {  // 64 lanes: at most the rest of this chunk + the next
+            m = cend + 32 - gn;
+            t = min(t, m);
+          }
           if (k < m && idx < cend) row[idx & 31] = rec;
           const uint32_t src = gb + m - 1;  // the last accepted entry
           pos = (uint32_t)__shfl((int)endq, (int)src);
@@ -211,7 +316,8 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
             if (pos >= len) break;                                   // iterator.go:115-118
             if (len - pos < 10) { gst = LSMGPU_BLK_TRUNC_HEADER; break; }
             uint32_t plen, klen, vlen;
-            read_hdr(blk + pos, plen, klen, vlen);                   // iterator.go:121
+            if (staged) read_hdr_lds(sd, sh + pos, plen, klen, vlen);  // iterator.go:121
+            else read_hdr(blk + pos, plen, klen, vlen);
             if ((klen | plen) == 0) break;                           // iterator.go:124-127
             if (gn == 0 && plen != 0) { gst = LSMGPU_BLK_FIRST_PLEN; break; }  // :129-133
             if (10 + plen > len) { gst = LSMGPU_BLK_PREFIX_OOB; break; }
@@ -241,6 +347,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
         // + kPlenFlag: the block holds prefix-compressed entries (K exceeds the stored key bytes)
         s_res[3][g] = gst | (gK != pos - 10 * gn - gV ? kPlenFlag : 0u);
         s_off[g] = off;
+        s_stg[g] = staged;
       }
     }
     __syncthreads();
@@ -250,6 +357,9 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
       V = s_res[2][tid];
       const uint32_t sw = s_res[3][tid];
       st = sw & ~kPlenFlag;
+    }
+    if (b < p.nblk && !scopy) {
+      const uint32_t sw = s_res[3][tid];
       uint64_t* t = p.wstat + 3ull * b;
       t[0] = n;
       t[1] = K;
@@ -395,7 +505,11 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     const uint32_t en = sat_add(on, in_ - n), ek = sat_add(ok, ik == 0xffffffffu ? ik : ik - K),
                    ev = sat_add(ov, iv - V);
     en_b = en;
-    if (!p.wfuse) {
+    if (scopy) {
+      s_cb[0][tid] = en;
+      s_cb[1][tid] = ek;
+      s_cb[2][tid] = ev;
+    } else if (!p.wfuse) {
       uint64_t* bs = p.wbase + 3ull * b;
       bs[0] = en;
       bs[1] = ek;
@@ -418,7 +532,32 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
         atomicOr(reinterpret_cast<unsigned long long*>(p.result + 5), 1ull);
     }
   }
-  if (!p.wfuse) return;
+  if (!p.wfuse) {
+    if constexpr (kStaged) {
+      // the staged walk's copy (p.wscopy): wave w copies block tile * 4 + w from its LDS slot
+      // (its records were flushed to p.wmeta by this wave), so the input is read once and no
+      // copy launch follows
+      if (scopy) {
+        __syncthreads();  // the bases (s_cb); the records in p.wmeta (workgroup scope)
+        const uint32_t bw = tile * TB + wave;
+        if (bw < p.nblk) {
+          const uint32_t* meta = p.wmeta + (uint64_t)bw * p.wcap;
+          const uint32_t pre = meta[min(lane, p.wcap - 1)];
+          const uint32_t off = s_off[wave];
+          const uint32_t nw = s_res[0][wave], Kw = s_res[1][wave], Vw = s_res[2][wave],
+                         sw = s_res[3][wave];
+          const uint64_t enw = s_cb[0][wave], ekw = s_cb[1][wave], evw = s_cb[2][wave];
+          if (s_stg[wave])
+            copy_block(p, bw, meta, pre, nw, Kw, Vw, sw, enw, ekw, evw, off, 0, 1, lane,
+                       LdsBytes{lds + TB * 32 * sizeof(uint32_t) + wave * kSlot, off & 15u});
+          else
+            copy_block(p, bw, meta, pre, nw, Kw, Vw, sw, enw, ekw, evw, off, 0, 1, lane,
+                       GlobalBytes{p.data + off});
+        }
+      }
+    }
+    return;
+  }
   if constexpr (KEEP) {
     if (!((p.mode & LSMGPU_MODE_VIEW) && p.view) || (p.ablate & 2)) return;  // mode 0: no view
     // each wave writes its 64 blocks' records -- consecutive in the output -- one lane per
@@ -550,9 +689,9 @@ __device__ __forceinline__ void entry_outputs(const DecodeParams& p, const uint3
   }
 }
 
-template <uint32_t J, uint32_t G, bool EO>  // EO: also the per-entry outputs (else entry_outputs)
+template <uint32_t J, uint32_t G, bool EO, typename Src>  // EO: also the per-entry outputs
 __device__ __forceinline__ void copy_entries(const DecodeParams& p, const uint32_t* meta,
-                                             const uint8_t* blk, uint8_t* kbase, uint8_t* vbase,
+                                             const Src& blk, uint8_t* kbase, uint8_t* vbase,
                                              uint32_t n, uint64_t en, uint64_t ek, uint64_t ev,
                                              uint32_t off, uint32_t sub, uint32_t split,
                                              bool mat, bool view, uint32_t lane, uint32_t pre) {
@@ -605,7 +744,7 @@ __device__ __forceinline__ void copy_entries(const DecodeParams& p, const uint32
         uint8_t* dst = key ? kbase : vbase;
         if (!dst) continue;
         const uint32_t s0 = key ? hp[i] + 10 : hp[i] + 10 + kl[i];
-        copy_piece16(dst + (key ? ko[i] : vo[i]), blk + s0, len, key ? q : q - kp[i]);
+        blk.piece(dst + (key ? ko[i] : vo[i]), s0, len, key ? q : q - kp[i]);
       }
     }
   }
@@ -647,25 +786,16 @@ __device__ __forceinline__ void copy_entries_plen(const DecodeParams& p, const u
   }
 }
 
-// K2: one wave per block (p.wsplit waves above 8 KiB).
-__global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
-  const uint32_t lane = lane_id();
-  // p.wsplit waves share a block (large blocks): wave `sub` takes passes sub, sub + wsplit, ...
-  const uint32_t wave = threadIdx.x >> 6, split = p.wsplit;
-  const uint32_t sub = wave % split;
-  const uint32_t b = uniform(blockIdx.x * (4 / split) + wave / split);
-  if (b >= p.nblk) return;
-  const uint32_t* meta = p.wmeta + (uint64_t)b * p.wcap;
-  // the first 64 metadata records, one per lane, requested beside the per-block loads below
-  // (one round trip fewer before the piece loads; records past the sentinel are never used)
-  const uint32_t pre = meta[min(lane, p.wcap - 1)];
-  const uint64_t* t = p.wstat + 3ull * b;
-  const uint32_t n = uniform((uint32_t)t[0]), K = uniform((uint32_t)t[1]),
-                 V = uniform((uint32_t)t[2]);
-  const uint32_t sw = uniform(p.wstatus[b]), st = sw & ~kPlenFlag;
-  const uint64_t* bs = p.wbase + 3ull * b;
-  const uint64_t en = uniform64(bs[0]), ek = uniform64(bs[1]), ev = uniform64(bs[2]);
-  const uint32_t off = uniform(p.blk_off[b]);
+// One block's share of the copy (wave `sub` of `split`): per-block outputs and result totals,
+// the capacity check, then the entries -- from the walk's records `meta` (`pre` = record `lane`),
+// the block's bytes read through `src` (prefix-compressed blocks always from global memory).
+template <typename Src>
+__device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, const uint32_t* meta,
+                                           uint32_t pre, uint32_t n, uint32_t K, uint32_t V,
+                                           uint32_t sw, uint64_t en, uint64_t ek, uint64_t ev,
+                                           uint32_t off, uint32_t sub, uint32_t split,
+                                           uint32_t lane, const Src& src) {
+  const uint32_t st = sw & ~kPlenFlag;
   if (lane == 0 && sub == 0) {
     if (p.blk_first) p.blk_first[b] = (uint32_t)en;
     if (p.blk_status) p.blk_status[b] = (int32_t)st;
@@ -694,7 +824,7 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
     return;
   }
   if (n == 0 || (p.ablate & 2)) return;
-  const uint8_t* blk = p.data + off;
+  const uint8_t* blk = p.data + off;  // (prefix-compressed blocks)
   uint8_t* kbase = p.key_data ? p.key_data + ek : nullptr;
   uint8_t* vbase = p.val_data ? p.val_data + ev : nullptr;
   // lanes per entry from this block's average entry (known after the walk): 8 for C2-like
@@ -714,12 +844,34 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   // the copy unchanged, 0.6038 vs 0.6042 ms, profiles/r04c; compiled into this kernel it also
   // raised the VGPRs from 44 to 90, 8 -> 5 waves per SIMD: removed)
   if (p.wj == 16 || (p.wj == 0 && avg > 128)) {
-    copy_entries<16, 2, true>(p, meta, blk, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
+    copy_entries<16, 2, true>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
   } else {
     entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
     if (mat)
-      copy_entries<8, 5, false>(p, meta, blk, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
+      copy_entries<8, 5, false>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
   }
+}
+
+// K2: one wave per block (p.wsplit waves above 8 KiB).
+__global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
+  const uint32_t lane = lane_id();
+  // p.wsplit waves share a block (large blocks): wave `sub` takes passes sub, sub + wsplit, ...
+  const uint32_t wave = threadIdx.x >> 6, split = p.wsplit;
+  const uint32_t sub = wave % split;
+  const uint32_t b = uniform(blockIdx.x * (4 / split) + wave / split);
+  if (b >= p.nblk) return;
+  const uint32_t* meta = p.wmeta + (uint64_t)b * p.wcap;
+  // the first 64 metadata records, one per lane, requested beside the per-block loads below
+  // (one round trip fewer before the piece loads; records past the sentinel are never used)
+  const uint32_t pre = meta[min(lane, p.wcap - 1)];
+  const uint64_t* t = p.wstat + 3ull * b;
+  const uint32_t n = uniform((uint32_t)t[0]), K = uniform((uint32_t)t[1]),
+                 V = uniform((uint32_t)t[2]);
+  const uint32_t sw = uniform(p.wstatus[b]);
+  const uint64_t* bs = p.wbase + 3ull * b;
+  const uint64_t en = uniform64(bs[0]), ek = uniform64(bs[1]), ev = uniform64(bs[2]);
+  const uint32_t off = uniform(p.blk_off[b]);
+  copy_block(p, b, meta, pre, n, K, V, sw, en, ek, ev, off, sub, split, lane, GlobalBytes{p.data + off});
 }
 
 
@@ -729,6 +881,12 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 128>), dim3((nblk + 127) / 128), dim3(256), 0, s, p);
   else if (p.wwalk == kWalkGroup && p.wlanes == 4)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 64>), dim3((nblk + 63) / 64), dim3(256), 0, s, p);
+  else if (p.wwalk == kWalkGroup && p.wlanes == 64 && p.wslot == 1)  // 4 KiB blocks: 7 WGs per CU
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 4, 32, kStageSlotSmall>), dim3((nblk + 3) / 4), dim3(256), 0, s, p);
+  else if (p.wwalk == kWalkGroup && p.wlanes == 64)
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 4>), dim3((nblk + 3) / 4), dim3(256), 0, s, p);
+  else if (p.wwalk == kWalkGroup && p.wlanes == 32)
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 8>), dim3((nblk + 7) / 8), dim3(256), 0, s, p);
   else if (p.wwalk == kWalkGroup && p.wlanes == 16)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 16>), dim3((nblk + 15) / 16), dim3(256), 0, s, p);
   else if (p.wwalk == kWalkGroup)
@@ -745,7 +903,8 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 256>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
   hipError_t e = hipGetLastError();
   if (e == hipSuccess && mid) e = hipEventRecord(mid, s);
-  if (e != hipSuccess || p.wfuse) return e;  // view-only: the walk wrote everything
+  // view-only, or the staged walk copying its blocks: the walk wrote everything
+  if (e != hipSuccess || p.wfuse || p.wscopy) return e;
   const uint32_t per_wg = 4 / p.wsplit;  // blocks per 4-wave workgroup
   hipLaunchKernelGGL(wsc_copy_kernel, dim3((nblk + per_wg - 1) / per_wg), dim3(256), 0, s, p);
   return hipGetLastError();

@@ -52,6 +52,8 @@ struct DecodeParams {
   uint32_t wchunk;          // lane walk: records per flushed chunk (16 or 32)
   uint32_t wkeep;           // view-only lane walk: records kept in LDS (kWalkLaneView)
   uint32_t wtile;           // lane walks: blocks (= threads) per workgroup, 192 or 256
+  uint32_t wscopy;          // 64-lane staged group walk: each wave copies its block from LDS
+  uint32_t wslot;           // 64-lane staged group walk: 0 = kStageSlot, 1 = kStageSlotSmall
 
 };
 
@@ -226,6 +228,9 @@ hipError_t launch_bloom_json(const BloomJson& p, hipStream_t s);
 // walk-scan-copy walk modes (DecodeParams::wwalk)
 constexpr int kWalkLane = 0;    // one lane per block, header by header from HBM
 constexpr int kWalkGroup = 2;   // wlanes lanes per block, speculative same-shape runs from HBM
+// the 64-lane group walk's LDS slot per block (bytes): 4 slots + rows leave 2 workgroups per CU
+constexpr uint32_t kStageSlot = 19456;
+constexpr uint32_t kStageSlotSmall = 4352;  // (LSMGPU_WSC_SLOT=small: C2's <= 4.2 KiB blocks)
 constexpr int kWalkLaneView = 3;  // view-only lane walk keeping each block's records in LDS
 constexpr uint32_t kViewRec = 33;  // records a kWalkLaneView LDS row keeps (more go to wmeta)
 // which decode path a batch takes: 0 register-lag (<= 4 KiB), 1 LDS-lag, 2 walk-scan-copy

@@ -505,11 +505,12 @@ def test_wsc_lanes_per_entry(codec, oracle, monkeypatch, lanes):
 
 
 @pytest.mark.parametrize("walk", ["lane", "lane16", "lane192", "lane_flush", "group", "group2",
-                                  "group4", "group16"])
+                                  "group4", "group16", "group32", "group64", "group64_copy", "group64s"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     """Walk-scan-copy's walks (LSMGPU_WSC_WALK): one lane per block from HBM, or 8 / 4
-    / 16 lanes per block guessing same-shape runs from HBM.  C2 / C3 / C4 (100 entries
+    / 16 / 32 lanes per block guessing same-shape runs from HBM (64: from the block staged in
+    LDS, blocks too long for the slot from HBM).  C2 / C3 / C4 (100 entries
     per block) blocks, short and tiny entries (> 64 per block), every KAT block (error statuses,
     terminators, plen > 0) at odd alignments, prefix-compressed random blocks, a ragged last
     tile and a block ending at the buffer's end (plus C5 32 KiB blocks for the HBM walks)."""
@@ -524,6 +525,12 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     elif walk == "lane_flush":  # view-only: records flushed and re-read (no LDS-kept rows)
         monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
         monkeypatch.setenv("LSMGPU_WSC_VIEWKEEP", "0")
+    elif walk == "group64s":  # the staged walk with 4.25 KiB slots (longer blocks from HBM)
+        monkeypatch.setenv("LSMGPU_WSC_WALK", "group64")
+        monkeypatch.setenv("LSMGPU_WSC_SLOT", "small")
+    elif walk == "group64_copy":  # the staged walk followed by the copy launch
+        monkeypatch.setenv("LSMGPU_WSC_WALK", "group64")
+        monkeypatch.setenv("LSMGPU_WSC_STAGECOPY", "0")
     else:
         monkeypatch.setenv("LSMGPU_WSC_WALK", walk)
     monkeypatch.setenv("LSMGPU_WSC_VIEWFUSE", "1")
@@ -611,7 +618,7 @@ def _block_entries(block):
     return out
 
 
-@pytest.mark.parametrize("walk", ["lane", "lane16", "lane192", "group"])
+@pytest.mark.parametrize("walk", ["lane", "lane16", "lane192", "group", "group32", "group64"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
     """Blocks built to defeat a header-pattern filter, decoded by every walk.  Keys and
