@@ -163,9 +163,12 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   // group walk of 64 lanes (TB = 4, one wave per block): the wave first copies its block into an
   // LDS slot with every load in flight, then walks it there (kStaged; blocks too long for a
   // slot walk from global memory)
-  constexpr bool kStaged = MODE == kWalkGroup && TB == 4;
+  // (SLOT = 0: the 64-lane walk reads global memory; its round is all scalar -- ballots,
+  // s_ff1, v_readlane -- instead of the narrower groups' LDS lane shuffles)
+  constexpr bool kWave64 = MODE == kWalkGroup && TB == 4;
+  constexpr bool kStaged = kWave64 && SLOT > 0;
   constexpr uint32_t kSlot = kStaged ? SLOT : 0u;
-  static_assert(SLOT % 16 == 0, "16-B chunks");
+  static_assert(SLOT % 16 == 0, "16-B chunks (0: no staging)");
   constexpr uint32_t kLdsBytes =
       MODE == kWalkGroup ? TB * 32 * sizeof(uint32_t) + TB * kSlot : kStageBytes;
   static_assert(MODE == kWalkGroup || kLdsBytes == kStageBytes,
@@ -179,10 +182,10 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   __shared__ uint32_t s_off[MODE == kWalkGroup ? TB : kThreads];  // each block's input offset
   constexpr uint32_t kRes = MODE == kWalkGroup ? TB : 1;
   __shared__ uint32_t s_res[4][kRes];  // group / wave walk: n, K, V, status per block
-  __shared__ uint32_t s_stg[kStaged ? TB : 1];  // the block is in its LDS slot
-  __shared__ uint32_t s_cb[3][kStaged ? TB : 1];  // p.wscopy: each block's output bases
+  __shared__ uint32_t s_stg[kRes];  // group walk: the block is in its LDS slot (kStaged)
+  __shared__ uint32_t s_cb[3][kWave64 ? TB : 1];  // p.wscopy: each block's output bases
   // the staged walk copying its own blocks (p.wscopy): no records for a copy launch
-  const bool scopy = kStaged && p.wscopy && !p.wfuse;
+  const bool scopy = kWave64 && p.wscopy && !p.wfuse;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t ntiles = (p.nblk + TB - 1) / TB;
   if (tid == 0) {
@@ -220,18 +223,21 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
       bool staged = false;
       if ((uint64_t)off + len > p.data_len) {
         gst = LSMGPU_BLK_RANGE;
+      } else if (p.ablate & 4) {  // (timing-only ablation: no walk, every block empty)
       } else {
         const uint8_t* blk = p.data + off;
-        // kStaged: the block's bytes [off & ~15, off + len) as 16-B chunks in the wave's slot,
-        // header q at byte sh + q (chunks past the end of the input load byte by byte)
-        const uint32_t sh = off & 15u;
-        staged = kStaged && sh + len + 16 <= kSlot;
+        // kStaged: the block's bytes [off, off + len) as (unaligned) 16-B chunks in the wave's
+        // slot, header q at byte q.  Nothing before off is read: the host pipeline's data
+        // pointer is biased (only [chunk start, data_len) is readable); a chunk past data_len
+        // loads byte by byte.
+        const uint32_t sh = 0;
+        staged = kStaged && len + 16 <= kSlot;
         const uint32_t* sd = reinterpret_cast<const uint32_t*>(lds + TB * 32 * sizeof(uint32_t) + g * kSlot);
         if constexpr (kStaged) {
           if (staged) {
-            const uint64_t a0 = (uint64_t)off - sh;
-            const uint32_t n16 = (sh + len + 15) >> 4;
-            const uint4* src = reinterpret_cast<const uint4*>(p.data + a0);
+            const uint64_t a0 = off;
+            const uint32_t n16 = (len + 15) >> 4;
+            const uint8_t* src = p.data + a0;
             uint4* dst = reinterpret_cast<uint4*>(lds + TB * 32 * sizeof(uint32_t) + g * kSlot);
             for (uint32_t c0 = 0; c0 < n16; c0 += 8 * L) {
               uint4 v[8];
@@ -241,10 +247,10 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
                 v[u] = make_uint4(0, 0, 0, 0);
                 if (c < n16) {
                   if (a0 + 16ull * c + 16 <= p.data_len) {
-                    v[u] = src[c];
+                    __builtin_memcpy(&v[u], src + 16 * c, 16);
                   } else {  // the input's last partial chunk
                     uint8_t t[16] = {};
-                    for (uint32_t j = 0; a0 + 16ull * c + j < p.data_len; j++) t[j] = p.data[a0 + 16ull * c + j];
+                    for (uint32_t j = 0; j < 16 && a0 + 16ull * c + j < p.data_len; j++) t[j] = src[16 * c + j];
                     __builtin_memcpy(&v[u], t, 16);
                   }
                 }
@@ -258,33 +264,52 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
         }
         uint32_t kref = 0xffffffffu, vref = 0, stride = 0;  // no shape yet: round 1 takes one
         uint32_t rounds = 0;
+        // p.wsub: a round is a window of L entries; after an odd-shaped entry only the lanes
+        // past the accepted ones guess again (sub-round), from the corrected position -- their
+        // guesses move by the odd entry's size difference, so the lines are already in L1 --
+        // and a new window (new lines) starts once all L lanes are accepted.  Lane k guesses
+        // window entry j = k - a (lanes below a idle).
+        uint32_t a = 0;
         for (;;) {
-          const uint32_t q = pos + k * stride;  // < 2^24: pos, stride < 2^17, k < 64
+          const bool act = k >= a;
+          const uint32_t j = k - a;
+          const uint32_t q = pos + j * stride;  // < 2^24 for active lanes: stride < 2^17, j < 64
           uint32_t plen = 1, klen = 0, vlen = 0;
           // default loads here: the copy after a small batch re-reads the lines from the
           // Infinity Cache (nt guesses: C4 walk 0.038 -> 0.043 ms, copy 0.032 -> 0.042 ms)
-          if (q + 10 <= len) {
+          if (act && q + 10 <= len) {
             if (staged) read_hdr_lds(sd, sh + q, plen, klen, vlen);
             else read_hdr(blk + q, plen, klen, vlen);
           }
           const uint32_t endq = q + 10 + klen + vlen;
           const bool fast = (klen != 0) & (plen == 0) & (endq <= len);
           const bool same = fast & (klen == kref) & (vlen == vref);
-          const uint64_t fb = (__ballot(fast) >> gb) & kMask;
-          const uint64_t sb = (__ballot(same) >> gb) & kMask;
+          const uint64_t wm = kMask >> a;  // the window's remaining lanes
+          const uint32_t La = L - a;
+          const uint64_t fb = (__ballot(fast) >> (gb + a)) & wm;
+          const uint64_t sb = (__ballot(same) >> (gb + a)) & wm;
           if (!(fb & 1u)) break;  // entry n itself needs the general loop (or the block ended)
-          uint32_t t = sb == kMask ? L : (uint32_t)__builtin_ctzll(~sb);  // leading same-shape run
-          uint32_t m = t + ((t < L && ((fb >> t) & 1u)) ? 1u : 0u);  // + one new shape
-          const uint32_t rec = q | ((gV + k * vref) << 16);
-          const uint32_t idx = gn + k, cend = (gn | 31u) + 1;  // end of the current chunk
-          if (L > 32 && gn + m > cend + 32) {  // 64 lanes: at most the rest of this chunk + the next
-            m = cend + 32 - gn;
+          uint32_t t = sb == wm ? La : (uint32_t)__builtin_ctzll(~sb);  // leading same-shape run
+          uint32_t m = t + ((t < La && ((fb >> t) & 1u)) ? 1u : 0u);  // + one new shape
+          const uint32_t rec = q | ((gV + j * vref) << 16);
+          const uint32_t idx = gn + j, cend = (gn | 31u) + 1;  // end of the current chunk
+          // 64 lanes: the run may cross one chunk boundary but must not complete the next chunk
+          // too (only the chunk ending at cend is flushed below)
+          if (L > 32 && gn + m >= cend + 32) {
+            m = cend + 31 - gn;
             t = min(t, m);
           }
-          if (k < m && idx < cend) row[idx & 31] = rec;
-          const uint32_t src = gb + m - 1;  // the last accepted entry
-          pos = (uint32_t)__shfl((int)endq, (int)src);
-          const uint32_t shape = (uint32_t)__shfl((int)(klen | (vlen << 16)), (int)src);
+          const bool acc = act && j < m;  // this lane's entry is accepted
+          if (acc && idx < cend) row[idx & 31] = rec;
+          const uint32_t src = gb + a + m - 1;  // the last accepted entry
+          uint32_t shape;
+          if constexpr (L == 64) {  // src is wave-uniform (from ballots)
+            pos = __builtin_amdgcn_readlane(endq, src);
+            shape = __builtin_amdgcn_readlane(klen | (vlen << 16), src);
+          } else {
+            pos = (uint32_t)__shfl((int)endq, (int)src);
+            shape = (uint32_t)__shfl((int)(klen | (vlen << 16)), (int)src);
+          }
           gK += t * kref + (m > t ? (shape & 0xffffu) : 0u);
           gV += t * vref + (m > t ? (shape >> 16) : 0u);
           gn += m;
@@ -303,7 +328,11 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
               reinterpret_cast<uint4*>(meta + cend - 32)[i] =
                   make_uint4(row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3]);
             __builtin_amdgcn_wave_barrier();  // the chunk is read before the next one fills
-            if (k < m && idx >= cend) row[idx & 31] = rec;
+            if (acc && idx >= cend) row[idx & 31] = rec;
+          }
+          if (p.wsub) {
+            a += m;
+            if (a >= L) a = 0;
           }
           // shapes do not repeat in this block (< 1.25 entries per round after 16 rounds): the
           // rest entry by entry.  A rate over many rounds, not a streak -- with thousands of
@@ -481,7 +510,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     }
     uint64_t* R = p.lb + (uint64_t)tile * 8;
     Tot ex{0, 0, 0};
-    if (tile > 0) {
+    if (tile > 0 && !(p.ablate & 1)) {  // (timing-only ablation 1: no look-back)
       store3(R, p.tag, tn, tk, tv, lane);
       ex = lookback(p.lb, tile, p.tag, lane, p.result);
     }
@@ -533,8 +562,8 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     }
   }
   if (!p.wfuse) {
-    if constexpr (kStaged) {
-      // the staged walk's copy (p.wscopy): wave w copies block tile * 4 + w from its LDS slot
+    if constexpr (kWave64) {
+      // the 64-lane walk's copy (p.wscopy): wave w copies block tile * 4 + w from its LDS slot
       // (its records were flushed to p.wmeta by this wave), so the input is read once and no
       // copy launch follows
       if (scopy) {
@@ -547,9 +576,9 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
           const uint32_t nw = s_res[0][wave], Kw = s_res[1][wave], Vw = s_res[2][wave],
                          sw = s_res[3][wave];
           const uint64_t enw = s_cb[0][wave], ekw = s_cb[1][wave], evw = s_cb[2][wave];
-          if (s_stg[wave])
+          if (kStaged && s_stg[wave])
             copy_block(p, bw, meta, pre, nw, Kw, Vw, sw, enw, ekw, evw, off, 0, 1, lane,
-                       LdsBytes{lds + TB * 32 * sizeof(uint32_t) + wave * kSlot, off & 15u});
+                       LdsBytes{lds + TB * 32 * sizeof(uint32_t) + wave * kSlot, 0u});
           else
             copy_block(p, bw, meta, pre, nw, Kw, Vw, sw, enw, ekw, evw, off, 0, 1, lane,
                        GlobalBytes{p.data + off});
@@ -881,6 +910,8 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 128>), dim3((nblk + 127) / 128), dim3(256), 0, s, p);
   else if (p.wwalk == kWalkGroup && p.wlanes == 4)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 64>), dim3((nblk + 63) / 64), dim3(256), 0, s, p);
+  else if (p.wwalk == kWalkGroup && p.wlanes == 64 && p.wslot == 2)  // from global memory
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 4, 32, 0>), dim3((nblk + 3) / 4), dim3(256), 0, s, p);
   else if (p.wwalk == kWalkGroup && p.wlanes == 64 && p.wslot == 1)  // 4 KiB blocks: 7 WGs per CU
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 4, 32, kStageSlotSmall>), dim3((nblk + 3) / 4), dim3(256), 0, s, p);
   else if (p.wwalk == kWalkGroup && p.wlanes == 64)

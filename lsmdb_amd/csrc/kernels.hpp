@@ -33,6 +33,7 @@ struct DecodeParams {
   uint64_t* result;         // 8 u64, zeroed before launch
   uint32_t tag;             // 24-bit epoch tag of this launch
   uint32_t ablate;          // timing-only diagnostics (LSMGPU_ABLATE): 1 no prefix, 2 no emit, 4 no walk
+                            // (walk-scan-copy: 1 no look-back, 2 no copy, 4 no group walk)
   uint32_t* census;         // residency census mode (launch_decode calibration), else nullptr
   uint64_t* stamps;         // per-phase s_memtime totals (LSMGPU_STAMPS diagnostics), else nullptr
   // walk-scan-copy path (decode_wsc.hip): per-entry metadata (2 words x wcap per block),
@@ -54,6 +55,7 @@ struct DecodeParams {
   uint32_t wtile;           // lane walks: blocks (= threads) per workgroup, 192 or 256
   uint32_t wscopy;          // 64-lane staged group walk: each wave copies its block from LDS
   uint32_t wslot;           // 64-lane staged group walk: 0 = kStageSlot, 1 = kStageSlotSmall
+  uint32_t wsub;            // group walk: odd-shaped entries re-guessed inside a round
 
 };
 

@@ -36,15 +36,14 @@ if has a; then
   run c2b 2
   run c2_t192b 2 LSMGPU_WSC_TILE=192
 fi
-if has g; then  # C4 (5,700 blocks: the group walk) -- lanes per block, copy waves per block
+if has g; then  # C4 (5,700 blocks: the group walk) -- lanes per block, sub-rounds, 64-lane walks
   run c4 4
-  run c4_g16 4 LSMGPU_WSC_WALK=group16
-  run c4_g32 4 LSMGPU_WSC_WALK=group32
-  run c4_g64 4 LSMGPU_WSC_WALK=group64
-  run c4_g64nc 4 LSMGPU_WSC_WALK=group64 LSMGPU_WSC_STAGECOPY=0
-  run c4_s4 4 LSMGPU_WSC_SPLIT=4
-  run c4_g32s4 4 LSMGPU_WSC_WALK=group32 LSMGPU_WSC_SPLIT=4
+  run c4_nosub 4 LSMGPU_WSC_SUB=0
+  run c4_g64g 4 LSMGPU_WSC_WALK=group64 LSMGPU_WSC_SLOT=none
+  run c4_g64gnc 4 LSMGPU_WSC_WALK=group64 LSMGPU_WSC_SLOT=none LSMGPU_WSC_STAGECOPY=0
+  run c4_g64gnosub 4 LSMGPU_WSC_WALK=group64 LSMGPU_WSC_SLOT=none LSMGPU_WSC_SUB=0
   run c4b 4
+  run c4_g64gb 4 LSMGPU_WSC_WALK=group64 LSMGPU_WSC_SLOT=none
 fi
 if has s; then  # C2 through the staged 64-lane walk with 4.25 KiB slots (one read of the input)
   run c2_g64s 2 LSMGPU_WSC_WALK=group64 LSMGPU_WSC_SLOT=small
