@@ -375,9 +375,10 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     // input) unless LSMGPU_WSC_STAGECOPY=0
     const char* sc_env = getenv("LSMGPU_WSC_STAGECOPY");
     p.wscopy = p.wwalk == kWalkGroup && p.wlanes == 64 && !p.wfuse && !(sc_env && atoi(sc_env) == 0);
-    // group walk: sub-rounds after an odd-shaped entry (LSMGPU_WSC_SUB=0: a new round instead)
+    // group walk: a new round after each odd-shaped entry; LSMGPU_WSC_SUB=1 re-guesses inside the
+    // round instead (sub-rounds: C4 walk 0.0407 vs 0.0384 ms, profiles/r04i -- not adopted)
     const char* sub_env = getenv("LSMGPU_WSC_SUB");
-    p.wsub = sub_env && atoi(sub_env) == 0 ? 0u : 1u;
+    p.wsub = sub_env && atoi(sub_env) == 1 ? 1u : 0u;
     const char* sl_env = getenv("LSMGPU_WSC_SLOT");  // A/B: "small" LDS slots (4.25 KiB)
     p.wslot = sl_env && sl_env[0] == 's' ? 1u : (sl_env && sl_env[0] == 'n' ? 2u : 0u);  // "none": global
     // d_result is zeroed by the walk kernel when a copy launch follows it (the copy's atomics

@@ -506,7 +506,7 @@ def test_wsc_lanes_per_entry(codec, oracle, monkeypatch, lanes):
 
 @pytest.mark.parametrize("walk", ["lane", "lane16", "lane192", "lane_flush", "group", "group2",
                                   "group4", "group16", "group32", "group64", "group64_copy", "group64s",
-                                  "group64g", "group64g_copy", "group_nosub", "group16_nosub"])
+                                  "group64g", "group64g_copy", "group_sub", "group16_sub"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     """Walk-scan-copy's walks (LSMGPU_WSC_WALK): one lane per block from HBM, or 8 / 4
@@ -529,9 +529,9 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     elif walk == "group64s":  # the staged walk with 4.25 KiB slots (longer blocks from HBM)
         monkeypatch.setenv("LSMGPU_WSC_WALK", "group64")
         monkeypatch.setenv("LSMGPU_WSC_SLOT", "small")
-    elif walk.endswith("_nosub"):  # a new round after every odd-shaped entry (round 3)
-        monkeypatch.setenv("LSMGPU_WSC_WALK", walk[:-6])
-        monkeypatch.setenv("LSMGPU_WSC_SUB", "0")
+    elif walk.endswith("_sub"):  # odd-shaped entries re-guessed inside the round
+        monkeypatch.setenv("LSMGPU_WSC_WALK", walk[:-4])
+        monkeypatch.setenv("LSMGPU_WSC_SUB", "1")
     elif walk.startswith("group64g"):  # 64 lanes from global memory (+ the copy launch)
         monkeypatch.setenv("LSMGPU_WSC_WALK", "group64")
         monkeypatch.setenv("LSMGPU_WSC_SLOT", "none")
@@ -627,7 +627,7 @@ def _block_entries(block):
 
 
 @pytest.mark.parametrize("walk", ["lane", "lane16", "lane192", "group", "group32", "group64",
-                                  "group64g", "group_nosub"])
+                                  "group64g", "group_sub"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
     """Blocks built to defeat a header-pattern filter, decoded by every walk.  Keys and
@@ -639,8 +639,8 @@ def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
     oracle's iterator does."""
     from lsmdb_amd.codec import MODE_MATERIALIZE, MODE_VIEW
     monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
-    monkeypatch.setenv("LSMGPU_WSC_WALK", "lane" if walk in ("lane16", "lane192") else walk.replace("_nosub", ""))
-    monkeypatch.setenv("LSMGPU_WSC_SUB", "0" if walk.endswith("_nosub") else "1")
+    monkeypatch.setenv("LSMGPU_WSC_WALK", "lane" if walk in ("lane16", "lane192") else walk.replace("_sub", ""))
+    monkeypatch.setenv("LSMGPU_WSC_SUB", "1" if walk.endswith("_sub") else "0")
     if walk == "group64g":
         monkeypatch.setenv("LSMGPU_WSC_WALK", "group64")
         monkeypatch.setenv("LSMGPU_WSC_SLOT", "none")
