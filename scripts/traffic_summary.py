@@ -21,6 +21,13 @@ import sys
 
 PIPELINE = ("lsmgpu::decode", "wsc_walk_kernel", "wsc_copy_kernel", "wsc_carry_kernel", "Tri64",
             "tile_decode_kernel", "fsw_kernel", "fsc_kernel", "onepass_kernel")
+# not part of a materialize decode: the view-only walk (kWalkLaneView = 3) that bench.py's
+# walk_fetch_bytes runs once to price the walk
+EXCLUDE = ("wsc_walk_kernel<3,",)
+
+
+def in_pipeline(name):
+    return any(k in name for k in PIPELINE) and not any(k in name for k in EXCLUDE)
 
 
 def per_launch(path, counters):
@@ -29,7 +36,7 @@ def per_launch(path, counters):
     vals = {}  # counter -> kernel name -> dispatch id -> value
     for r in csv.DictReader(open(path)):
         name, c = r["Kernel_Name"], r["Counter_Name"]
-        if c in counters and any(k in name for k in PIPELINE):
+        if c in counters and in_pipeline(name):
             d = vals.setdefault(c, {}).setdefault(name, {})
             d[int(r["Dispatch_Id"])] = d.get(int(r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
     out = {}
@@ -46,7 +53,7 @@ def kernels(path):
     names = []
     for r in csv.DictReader(open(path)):
         n = r["Kernel_Name"]
-        if any(k in n for k in PIPELINE):
+        if in_pipeline(n):
             short = n.split("(")[0][:90]
             if short not in names:
                 names.append(short)
