@@ -379,6 +379,15 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     // round instead (sub-rounds: C4 walk 0.0407 vs 0.0384 ms, profiles/r04i -- not adopted)
     const char* sub_env = getenv("LSMGPU_WSC_SUB");
     p.wsub = sub_env && atoi(sub_env) == 1 ? 1u : 0u;
+    // group walk: the round's two lane exchanges through LDS shuffles; LSMGPU_WSC_DPP=1 uses
+    // DPP OR-reductions instead (C4 walk 0.0395 vs 0.0392-0.0397 ms, profiles/r04l: no gain)
+    const char* dpp_env = getenv("LSMGPU_WSC_DPP");
+    p.wdpp = dpp_env && atoi(dpp_env) == 1 ? 1u : 0u;
+    // view-only lane walk: each pass's entry owners by a scatter of block starts + a DPP max-scan
+    // (C2 view 0.2677 / 0.2671 -> 0.2595 / 0.2604 ms, profiles/r04l); LSMGPU_WSC_VIEWSCAN=0: the
+    // 6-step lane-shuffle binary search
+    const char* vs_env = getenv("LSMGPU_WSC_VIEWSCAN");
+    p.wview = vs_env && atoi(vs_env) == 0 ? 0u : 1u;
     const char* sl_env = getenv("LSMGPU_WSC_SLOT");  // A/B: "small" LDS slots (4.25 KiB)
     p.wslot = sl_env && sl_env[0] == 's' ? 1u : (sl_env && sl_env[0] == 'n' ? 2u : 0u);  // "none": global
     // d_result is zeroed by the walk kernel when a copy launch follows it (the copy's atomics

@@ -117,6 +117,18 @@ __device__ __forceinline__ uint32_t wave_scan_sat(uint32_t v, uint32_t lane) {
   const uint32_t row = lane >> 4;
   return sat_add(v, row == 0 ? 0u : row == 1 ? r0 : row == 2 ? r1 : r2);
 }
+// Inclusive max-scan over the wave (DPP row_shr inside 16-lane rows, rows through v_readlane).
+__device__ __forceinline__ uint32_t wave_scan_max(uint32_t v, uint32_t lane) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true));
+  const uint32_t r0 = __builtin_amdgcn_readlane(v, 15);
+  const uint32_t r1 = max(r0, __builtin_amdgcn_readlane(v, 31));
+  const uint32_t r2 = max(r1, __builtin_amdgcn_readlane(v, 47));
+  const uint32_t row = lane >> 4;
+  return max(v, row == 0 ? 0u : row == 1 ? r0 : row == 2 ? r1 : r2);
+}
 __device__ __forceinline__ uint32_t wave_sum_sat(uint32_t v) {  // uniform result
   v = row_incl_sat(v);
   return sat_add(sat_add(__builtin_amdgcn_readlane(v, 15), __builtin_amdgcn_readlane(v, 31)),

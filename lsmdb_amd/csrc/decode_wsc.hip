@@ -63,6 +63,17 @@ __device__ __forceinline__ void read_hdr_lds(const uint32_t* d, uint32_t o, uint
   vlen = __builtin_amdgcn_perm(0u, y, 0x0c0c0001u);
 }
 
+// OR over each aligned group of L (2..16) lanes, every lane of the group receiving it: DPP
+// quad_perm [1,0,3,2] and [2,3,0,1], row_half_mirror (lane i <-> 7 - i), row_mirror (i <-> 15 - i)
+template <uint32_t L>
+__device__ __forceinline__ uint32_t group_or(uint32_t x) {
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0xB1, 0xf, 0xf, true);
+  if constexpr (L >= 4) x |= (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x4E, 0xf, 0xf, true);
+  if constexpr (L >= 8) x |= (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x141, 0xf, 0xf, true);
+  if constexpr (L >= 16) x |= (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x140, 0xf, 0xf, true);
+  return x;
+}
+
 }  // namespace
 
 // Per-entry metadata of the walk: one u32 record {header pos | value offset << 16} per entry
@@ -184,6 +195,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   __shared__ uint32_t s_res[4][kRes];  // group / wave walk: n, K, V, status per block
   __shared__ uint32_t s_stg[kRes];  // group walk: the block is in its LDS slot (kStaged)
   __shared__ uint32_t s_cb[3][kWave64 ? TB : 1];  // p.wscopy: each block's output bases
+  __shared__ uint32_t s_mark[KEEP ? kWaves : 1][64];  // kWalkLaneView, p.wview: owner marks
   // the staged walk copying its own blocks (p.wscopy): no records for a copy launch
   const bool scopy = kWave64 && p.wscopy && !p.wfuse;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
@@ -306,6 +318,12 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
           if constexpr (L == 64) {  // src is wave-uniform (from ballots)
             pos = __builtin_amdgcn_readlane(endq, src);
             shape = __builtin_amdgcn_readlane(klen | (vlen << 16), src);
+          } else if (L <= 16 && p.wdpp) {
+            // the group's OR of the one lane's values by DPP (quad swaps, half-row / row
+            // mirrors) -- no LDS round trip on the round's dependent chain
+            const bool me = k == src - gb;
+            pos = group_or<L>(me ? endq : 0u);
+            shape = group_or<L>(me ? (klen | (vlen << 16)) : 0u);
           } else {
             pos = (uint32_t)__shfl((int)endq, (int)src);
             shape = (uint32_t)__shfl((int)(klen | (vlen << 16)), (int)src);
@@ -409,7 +427,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
       len = p.blk_len[b];
       s_off[tid] = off;
     }
-    bool done = !valid;
+    bool done = !valid || (p.ablate & 4);  // (timing-only ablation 4: no walk)
     if (valid && (uint64_t)off + len > p.data_len) {
       st = LSMGPU_BLK_RANGE;
       done = true;
@@ -600,14 +618,33 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     const uint32_t T = __builtin_amdgcn_readlane(in_, 63);  // the wave's entries (no saturation:
                                                            // <= 64 x 6,554)
     const uint64_t ew = __builtin_amdgcn_readlane(en_b, 0);  // the wave's first output entry
+    // p.wview: the owner of each entry of a pass by one scatter and a max-scan instead -- every
+    // block with entries marks (lane + 1) at its first entry's slot of the pass, and a DPP
+    // max-scan carries the marks forward (the previous pass's last owner carried in)
+    uint32_t* const mk = s_mark[KEEP ? wave : 0];
+    if (p.wview) {
+      mk[lane] = 0;
+      wave_lds_fence();
+    }
+    uint32_t carry = 0;
     for (uint32_t c0 = 0; c0 < T; c0 += 64) {
       const uint32_t f = c0 + lane;
       uint32_t L = 0;
+      if (p.wview) {
+        if (n > 0 && pw >= c0 && pw < c0 + 64) mk[pw - c0] = lane + 1;
+        wave_lds_fence();
+        const uint32_t v = max(wave_scan_max(mk[lane], lane), carry);
+        mk[lane] = 0;  // for the next pass (this lane read its slot above)
+        wave_lds_fence();
+        carry = __builtin_amdgcn_readlane(v, 63);
+        L = v - 1;
+      } else {
 #pragma unroll
-      for (uint32_t st = 32; st >= 1; st >>= 1) {
-        const uint32_t cand = L + st;
-        const uint32_t pc = (uint32_t)__shfl((int)pw, (int)min(cand, 63u));
-        if (cand < 64 && pc <= f) L = cand;
+        for (uint32_t st = 32; st >= 1; st >>= 1) {
+          const uint32_t cand = L + st;
+          const uint32_t pc = (uint32_t)__shfl((int)pw, (int)min(cand, 63u));
+          if (cand < 64 && pc <= f) L = cand;
+        }
       }
       const uint32_t pL = (uint32_t)__shfl((int)pw, (int)L), nL = (uint32_t)__shfl((int)n, (int)L);
       const uint32_t offL = (uint32_t)__shfl((int)off_b, (int)L);

@@ -56,6 +56,8 @@ struct DecodeParams {
   uint32_t wscopy;          // 64-lane staged group walk: each wave copies its block from LDS
   uint32_t wslot;           // 64-lane staged group walk: 0 = kStageSlot, 1 = kStageSlotSmall
   uint32_t wsub;            // group walk: odd-shaped entries re-guessed inside a round
+  uint32_t wview;           // kWalkLaneView: owners by scatter + max-scan (else binary search)
+  uint32_t wdpp;            // group walk (<= 16 lanes): round results by DPP (else LDS shuffles)
 
 };
 

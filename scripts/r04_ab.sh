@@ -2,7 +2,7 @@
 # Round-4 same-box A/B: walk-scan-copy knobs (flush chunk), the E2E host pipeline through the C
 # ABI, and the other configs.  (The one-pass decode's phase stamps of profiles/r04c came from
 # this script's removed "s" part.)
-# Usage (on the GPU box): bash scripts/r04_ab.sh <tag> [parts]   parts: any of t a g s e c (default all)
+# Usage (on the GPU box): bash scripts/r04_ab.sh <tag> [parts]   parts: any of t a g s v e c (default all)
 set -o pipefail
 T=${1:-r04ab}
 PARTS=${2:-"t a e c"}
@@ -36,18 +36,22 @@ if has a; then
   run c2b 2
   run c2_t192b 2 LSMGPU_WSC_TILE=192
 fi
-if has g; then  # C4 (5,700 blocks: the group walk) -- lanes per block, sub-rounds, 64-lane walks
+if has g; then  # C4 (5,700 blocks: the group walk) -- lane exchange by DPP or LDS shuffles
   run c4 4
-  run c4_nosub 4 LSMGPU_WSC_SUB=0
-  run c4_g64g 4 LSMGPU_WSC_WALK=group64 LSMGPU_WSC_SLOT=none
-  run c4_g64gnc 4 LSMGPU_WSC_WALK=group64 LSMGPU_WSC_SLOT=none LSMGPU_WSC_STAGECOPY=0
-  run c4_g64gnosub 4 LSMGPU_WSC_WALK=group64 LSMGPU_WSC_SLOT=none LSMGPU_WSC_SUB=0
+  run c4_nodpp 4 LSMGPU_WSC_DPP=0
+  run c4_g16 4 LSMGPU_WSC_WALK=group16
   run c4b 4
-  run c4_g64gb 4 LSMGPU_WSC_WALK=group64 LSMGPU_WSC_SLOT=none
+  run c4_nodppb 4 LSMGPU_WSC_DPP=0
 fi
 if has s; then  # C2 through the staged 64-lane walk with 4.25 KiB slots (one read of the input)
   run c2_g64s 2 LSMGPU_WSC_WALK=group64 LSMGPU_WSC_SLOT=small
   run c2_g64snc 2 LSMGPU_WSC_WALK=group64 LSMGPU_WSC_SLOT=small LSMGPU_WSC_STAGECOPY=0
+fi
+if has v; then  # C2 view epilogue: owners by binary search vs scatter + max-scan
+  run c2 2
+  run c2_vs 2 LSMGPU_WSC_VIEWSCAN=1
+  run c2b 2
+  run c2_vsb 2 LSMGPU_WSC_VIEWSCAN=1
 fi
 if has e; then
   timeout -k 10 300 python scripts/e2e_abi.py > $O/e2e.json 2> $O/e2e.err || { tail -20 $O/e2e.err; exit 1; }

@@ -504,9 +504,10 @@ def test_wsc_lanes_per_entry(codec, oracle, monkeypatch, lanes):
     _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln), f"J={lanes}")
 
 
-@pytest.mark.parametrize("walk", ["lane", "lane16", "lane192", "lane_flush", "group", "group2",
+@pytest.mark.parametrize("walk", ["lane", "lane16", "lane192", "lane_flush", "lane_viewsearch", "group", "group2",
                                   "group4", "group16", "group32", "group64", "group64_copy", "group64s",
-                                  "group64g", "group64g_copy", "group_sub", "group16_sub"])
+                                  "group64g", "group64g_copy", "group_sub", "group16_sub",
+                                  "group_dpp"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     """Walk-scan-copy's walks (LSMGPU_WSC_WALK): one lane per block from HBM, or 8 / 4
@@ -523,12 +524,18 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     elif walk == "lane192":  # lane-walk workgroups of 192 blocks
         monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
         monkeypatch.setenv("LSMGPU_WSC_TILE", "192")
+    elif walk == "lane_viewsearch":  # view-only: owners by lane-shuffle binary search
+        monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
+        monkeypatch.setenv("LSMGPU_WSC_VIEWSCAN", "0")
     elif walk == "lane_flush":  # view-only: records flushed and re-read (no LDS-kept rows)
         monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
         monkeypatch.setenv("LSMGPU_WSC_VIEWKEEP", "0")
     elif walk == "group64s":  # the staged walk with 4.25 KiB slots (longer blocks from HBM)
         monkeypatch.setenv("LSMGPU_WSC_WALK", "group64")
         monkeypatch.setenv("LSMGPU_WSC_SLOT", "small")
+    elif walk == "group_dpp":  # the group's lane exchange by DPP OR-reductions
+        monkeypatch.setenv("LSMGPU_WSC_WALK", "group")
+        monkeypatch.setenv("LSMGPU_WSC_DPP", "1")
     elif walk.endswith("_sub"):  # odd-shaped entries re-guessed inside the round
         monkeypatch.setenv("LSMGPU_WSC_WALK", walk[:-4])
         monkeypatch.setenv("LSMGPU_WSC_SUB", "1")
