@@ -195,7 +195,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   __shared__ uint32_t s_res[4][kRes];  // group / wave walk: n, K, V, status per block
   __shared__ uint32_t s_stg[kRes];  // group walk: the block is in its LDS slot (kStaged)
   __shared__ uint32_t s_cb[3][kWave64 ? TB : 1];  // p.wscopy: each block's output bases
-  __shared__ uint32_t s_mark[KEEP ? kWaves : 1][64];  // kWalkLaneView, p.wview: owner marks
+  __shared__ uint32_t s_mark[KEEP ? kWaves : 1][128];  // kWalkLaneView, p.wview: owner marks
   // the staged walk copying its own blocks (p.wscopy): no records for a copy launch
   const bool scopy = kWave64 && p.wscopy && !p.wfuse;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
@@ -608,9 +608,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   if constexpr (KEEP) {
     if (!((p.mode & LSMGPU_MODE_VIEW) && p.view) || (p.ablate & 2)) return;  // mode 0: no view
     // each wave writes its 64 blocks' records -- consecutive in the output -- one lane per
-    // entry, 64 consecutive 8-B records per store instruction, from the rows its lanes filled:
-    // flat entry f of the wave belongs to the last block L whose wave-exclusive first entry
-    // (pw, lane L) is <= f (6 lane-shuffle steps)
+    // entry, 64 consecutive 8-B records per store instruction, from the rows its lanes filled
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // rows (and any spill) written
     __builtin_amdgcn_wave_barrier();
     const uint32_t wb0 = tile * TB + wave * 64;
@@ -618,39 +616,13 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     const uint32_t T = __builtin_amdgcn_readlane(in_, 63);  // the wave's entries (no saturation:
                                                            // <= 64 x 6,554)
     const uint64_t ew = __builtin_amdgcn_readlane(en_b, 0);  // the wave's first output entry
-    // p.wview: the owner of each entry of a pass by one scatter and a max-scan instead -- every
-    // block with entries marks (lane + 1) at its first entry's slot of the pass, and a DPP
-    // max-scan carries the marks forward (the previous pass's last owner carried in)
-    uint32_t* const mk = s_mark[KEEP ? wave : 0];
-    if (p.wview) {
-      mk[lane] = 0;
-      wave_lds_fence();
-    }
-    uint32_t carry = 0;
-    for (uint32_t c0 = 0; c0 < T; c0 += 64) {
-      const uint32_t f = c0 + lane;
-      uint32_t L = 0;
-      if (p.wview) {
-        if (n > 0 && pw >= c0 && pw < c0 + 64) mk[pw - c0] = lane + 1;
-        wave_lds_fence();
-        const uint32_t v = max(wave_scan_max(mk[lane], lane), carry);
-        mk[lane] = 0;  // for the next pass (this lane read its slot above)
-        wave_lds_fence();
-        carry = __builtin_amdgcn_readlane(v, 63);
-        L = v - 1;
-      } else {
-#pragma unroll
-        for (uint32_t st = 32; st >= 1; st >>= 1) {
-          const uint32_t cand = L + st;
-          const uint32_t pc = (uint32_t)__shfl((int)pw, (int)min(cand, 63u));
-          if (cand < 64 && pc <= f) L = cand;
-        }
-      }
+    // entry f of the wave (owner lane L): its 8-B view record from L's LDS row (or the spill)
+    auto emit = [&](uint32_t f, uint32_t L) {
       const uint32_t pL = (uint32_t)__shfl((int)pw, (int)L), nL = (uint32_t)__shfl((int)n, (int)L);
       const uint32_t offL = (uint32_t)__shfl((int)off_b, (int)L);
-      if (f >= T) continue;
+      if (f >= T) return;
       const uint64_t bend = ew + pL + nL;
-      if (!(bend <= p.ent_cap && bend <= 0xffffffffull)) continue;  // reported (result[5])
+      if (!(bend <= p.ent_cap && bend <= 0xffffffffull)) return;  // reported (result[5])
       const uint32_t e = f - pL;
       const uint32_t* rw = stage + (wave * 64 + L) * kStage;
       const uint32_t* gl = p.wmeta + (uint64_t)(wb0 + L) * p.wcap;
@@ -659,6 +631,43 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
       const uint32_t hp = m0 & 0xffffu, vl = (m1 >> 16) - (m0 >> 16);
       const uint32_t kl = (m1 & 0xffffu) - hp - 10 - vl;  // stored key bytes
       p.view[ew + f] = (uint64_t)(offL + hp + 10) | ((uint64_t)kl << 32) | ((uint64_t)vl << 48);
+    };
+    if (p.wview) {
+      // owners by one scatter and a max-scan, two passes (128 entries) per trip: every block
+      // with entries marks (lane + 1) at its first entry's slot, a DPP max-scan carries the
+      // marks forward (the previous pass's last owner carried in)
+      uint32_t* const mk = s_mark[KEEP ? wave : 0];
+      mk[lane] = 0;
+      mk[64 + lane] = 0;
+      wave_lds_fence();
+      uint32_t carry = 0;
+      for (uint32_t c0 = 0; c0 < T; c0 += 128) {
+        if (n > 0 && pw >= c0 && pw < c0 + 128) mk[pw - c0] = lane + 1;
+        wave_lds_fence();
+        const uint32_t a0 = mk[lane], a1 = mk[64 + lane];
+        mk[lane] = 0;  // for the next trip (this lane read its slots above)
+        mk[64 + lane] = 0;
+        const uint32_t v0 = max(wave_scan_max(a0, lane), carry);
+        const uint32_t v1 = max(wave_scan_max(a1, lane), __builtin_amdgcn_readlane(v0, 63));
+        carry = __builtin_amdgcn_readlane(v1, 63);
+        wave_lds_fence();
+        emit(c0 + lane, v0 - 1);
+        emit(c0 + 64 + lane, v1 - 1);
+      }
+    } else {
+      // the owner of entry f: the last block L whose wave-exclusive first entry (pw, lane L) is
+      // <= f (6 lane-shuffle steps)
+      for (uint32_t c0 = 0; c0 < T; c0 += 64) {
+        const uint32_t f = c0 + lane;
+        uint32_t L = 0;
+#pragma unroll
+        for (uint32_t st = 32; st >= 1; st >>= 1) {
+          const uint32_t cand = L + st;
+          const uint32_t pc = (uint32_t)__shfl((int)pw, (int)min(cand, 63u));
+          if (cand < 64 && pc <= f) L = cand;
+        }
+        emit(f, L);
+      }
     }
     return;
   }

@@ -49,9 +49,9 @@ if has s; then  # C2 through the staged 64-lane walk with 4.25 KiB slots (one re
 fi
 if has v; then  # C2 view epilogue: owners by binary search vs scatter + max-scan
   run c2 2
-  run c2_vs 2 LSMGPU_WSC_VIEWSCAN=1
+  run c2_vsearch 2 LSMGPU_WSC_VIEWSCAN=0
   run c2b 2
-  run c2_vsb 2 LSMGPU_WSC_VIEWSCAN=1
+  run c2_vsearchb 2 LSMGPU_WSC_VIEWSCAN=0
 fi
 if has e; then
   timeout -k 10 300 python scripts/e2e_abi.py > $O/e2e.json 2> $O/e2e.err || { tail -20 $O/e2e.err; exit 1; }
