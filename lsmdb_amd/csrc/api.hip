@@ -86,10 +86,18 @@ struct lsmgpu_ctx {
   uint64_t* h_chunk_res = nullptr;  // pinned, 8 u64 per slot
 };
 
-#define HIPC(x)                                   \
-  do {                                            \
-    hipError_t _e = (x);                          \
-    if (_e != hipSuccess) return LSMGPU_ERR_HIP;  \
+// LSMGPU_DEBUG_ERR=1: the failing HIP call and its error on stderr (diagnostics)
+static void report_hip_error(const char* what, hipError_t e, int line) {
+  static const bool on = getenv("LSMGPU_DEBUG_ERR") != nullptr;
+  if (on) fprintf(stderr, "lsmgpu: %s -> %s (api.hip:%d)\n", what, hipGetErrorString(e), line);
+}
+#define HIPC(x)                                    \
+  do {                                             \
+    hipError_t _e = (x);                           \
+    if (_e != hipSuccess) {                        \
+      report_hip_error(#x, _e, __LINE__);          \
+      return LSMGPU_ERR_HIP;                       \
+    }                                              \
   } while (0)
 
 extern "C" {
