@@ -36,12 +36,9 @@ if has a; then
   run c2b 2
   run c2_t192b 2 LSMGPU_WSC_TILE=192
 fi
-if has g; then  # C4 (5,700 blocks: the group walk) -- lane exchange by DPP or LDS shuffles
+if has g; then  # C4 (5,700 blocks: the group walk) -- one or two walk directions
   run c4 4
-  run c4_nodpp 4 LSMGPU_WSC_DPP=0
-  run c4_g16 4 LSMGPU_WSC_WALK=group16
   run c4b 4
-  run c4_nodppb 4 LSMGPU_WSC_DPP=0
 fi
 if has s; then  # C2 through the staged 64-lane walk with 4.25 KiB slots (one read of the input)
   run c2_g64s 2 LSMGPU_WSC_WALK=group64 LSMGPU_WSC_SLOT=small
