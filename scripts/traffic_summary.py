@@ -20,7 +20,7 @@ import os
 import sys
 
 PIPELINE = ("lsmgpu::decode", "wsc_walk_kernel", "wsc_copy_kernel", "wsc_carry_kernel", "Tri64",
-            "tile_decode_kernel", "fsw_kernel", "fsc_kernel", "onepass_kernel")
+            "tile_decode_kernel", "fsw_kernel", "fsc_kernel")
 # not part of a materialize decode: the view-only walk (kWalkLaneView = 3) that bench.py's
 # walk_fetch_bytes runs once to price the walk
 EXCLUDE = ("wsc_walk_kernel<3,",)

@@ -5,7 +5,7 @@
 set -o pipefail
 T=${1:-wscc}
 shift
-WALKS=${*:-stream lane group group4 group16}
+WALKS=${*:-lane group group4 group16}
 mkdir -p gpurun_out/$T
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fsc.py -x -q --timeout 120 --timeout-method thread > gpurun_out/$T/tests.log 2>&1 || { tail -40 gpurun_out/$T/tests.log; exit 1; }
 tail -2 gpurun_out/$T/tests.log
