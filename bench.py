@@ -257,12 +257,16 @@ def walk_fetch_bytes(torch, w, view, blk_first) -> int:
     position, klen, vlen per entry) and the block list, on the device.  For C2's 129-B entries
     this is every line of the input; for C3's 1,101-B entries about 4 lines of a block's 26."""
     n = int(blk_first[-1].item())
+    bf = blk_first.to(torch.int64)
+    # a wrong decode must raise here, not fault the queue in the gathers below
+    if (n != w.get("n", n) or n > view.numel() or int(bf[0].item()) != 0
+            or bool((bf[1:] < bf[:-1]).any().item())):
+        raise RuntimeError(f"view decode returned an invalid block index (n={n}, expected {w.get('n')})")
     v = view[:n].to(torch.int64)
     kp = v & 0xFFFFFFFF
     kl = (v >> 32) & 0xFFFF
     vl = (v >> 48) & 0xFFFF
     heads = [kp - 10]
-    bf = blk_first.to(torch.int64)
     cnt = bf[1:] - bf[:-1]
     off = w["d_off"].to(torch.int64) & 0xFFFFFFFF
     ln = w["d_len"].to(torch.int64) & 0xFFFFFFFF

@@ -25,8 +25,10 @@ extern "C" {
 #endif
 
 /* 2 (round 4): size queries (decode with every output pointer NULL, encode with out == NULL),
- * LSMGPU_ERR_CORRUPT, stream probe kinds 4-7 and its argument checks. */
-#define LSMGPU_ABI_VERSION 2
+ * LSMGPU_ERR_CORRUPT, stream probe kinds 4-7 and its argument checks.
+ * 3 (round 5): lsmgpu_host_register is refcounted per page segment (overlapping and re-used
+ * ranges), LSMGPU_ERR_HOST_PINNED, unregister of an unknown pointer is LSMGPU_ERR_ARG. */
+#define LSMGPU_ABI_VERSION 3
 
 /* ---- call status ---- */
 #define LSMGPU_OK 0
@@ -41,6 +43,9 @@ extern "C" {
 #define LSMGPU_ERR_NO_DEVICE 9  /* no HIP device / bad device index                            */
 #define LSMGPU_ERR_CORRUPT 10   /* compaction input: a block with a non-OK LSMGPU_BLK_* status, or
                                    a table whose keys are not in CompareKeys order              */
+#define LSMGPU_ERR_HOST_PINNED 11 /* host_register: the range overlaps memory page-locked outside
+                                   this library (hipHostMalloc, the caller's hipHostRegister);
+                                   nothing was registered -- such memory needs no registration */
 
 /* ---- per-block decode status (lsmgpu_decoded.blk_status) ---- */
 #define LSMGPU_BLK_OK 0             /* terminator, or pos >= len (iterator.go:115-118,124-127) */
@@ -125,9 +130,20 @@ int lsmgpu_decode_blocks(lsmgpu_ctx* ctx, const uint8_t* data, uint64_t data_len
 
 /* Host-memory calls (data_on_device = 0) with blocks sorted by offset are pipelined: chunks of
  * ~64 MiB (LSMGPU_HOST_CHUNK) are copied in, decoded and copied out on three streams at once.
- * DMA runs at PCIe rate only from page-locked memory: pin the mmap'd .sst (and large output
- * arrays) once with lsmgpu_host_register (hipHostRegister; read-only mappings accepted) and
- * unpin with lsmgpu_host_unregister before munmap.  Memory already pinned is accepted. */
+ * DMA runs at PCIe rate only from page-locked memory: pin the .sst bytes (an mmap -- read-only
+ * mappings are pinned read-only -- or LoadToRAM's heap buffer, table.go:117-123,329-338) and
+ * large output arrays with lsmgpu_host_register, unpin with lsmgpu_host_unregister(p) (the same
+ * pointer) before the memory is freed or unmapped.
+ * Pinning is page-granular.  The library keeps one process-wide registry of page-aligned
+ * segments, each pinned once: a range pins only its pages no earlier registration covers and
+ * references every segment it overlaps, so ranges may share pages, nest, repeat and come back
+ * at re-used addresses; a segment is unpinned when its last range is unregistered.  Every host
+ * copy the library makes is cut at segment borders.  Register / unregister are thread-safe.
+ * Returns LSMGPU_ERR_HOST_PINNED (nothing registered) for memory already page-locked outside
+ * the library, and LSMGPU_ERR_HIP when the OS refuses (e.g. RLIMIT_MEMLOCK): the host calls then
+ * work on the memory as it is, staged by the runtime.  lsmgpu_host_unregister of a pointer with
+ * no registration returns LSMGPU_ERR_ARG.  Unregister only when no call using memory in the same
+ * pages is running. */
 int lsmgpu_host_register(lsmgpu_ctx* ctx, void* p, uint64_t bytes);
 int lsmgpu_host_unregister(lsmgpu_ctx* ctx, void* p);
 

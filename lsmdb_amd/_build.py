@@ -9,7 +9,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "lsmdb_amd", "csrc")
 LIB = os.path.join(ROOT, "lsmdb_amd", "liblsmgpu.so")
 SOURCES = ["api.hip", "decode.hip", "decode_wsc.hip", "encode.hip", "open_tables.hip", "merge.hip", "bloom.hip", "probe.hip"]
-HEADERS = ["codec_common.hpp", "decode_common.hpp", "kernels.hpp", os.path.join("..", "..", "include", "lsmgpu.h")]
+HEADERS = ["codec_common.hpp", "decode_common.hpp", "kernels.hpp", "pin_registry.hpp",
+           os.path.join("..", "..", "include", "lsmgpu.h")]
 ARCH = os.environ.get("LSMGPU_ARCH", "gfx950")
 
 
@@ -21,32 +22,43 @@ def _stale(target: str, deps: list[str]) -> bool:
 
 
 def build_lib(force: bool = False, verbose: bool = True) -> str:
-    """Each source compiled to its own object in parallel (build/), then one link."""
+    """Each source compiled to its own object in parallel, then one link.  Every flavor (the
+    product library, the LSMGPU_BUILD_STAMPS diagnostic one) has its own object directory, and
+    objects and the library are written to temporary names renamed into place, so two builds at
+    once (two bench ranks, two test processes) never read each other's half-written files."""
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
-    if not force and not _stale(LIB, deps):
-        return LIB
     flags = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall"]
-    lib = LIB
+    lib, flavor = LIB, "default"
     if os.environ.get("LSMGPU_BUILD_STAMPS"):  # diagnostic build: per-phase s_memtime stamps
         flags.append("-DLSMGPU_STAMPS")
-        lib = LIB.replace("liblsmgpu.so", "liblsmgpu_stamps.so")
-    objdir = os.path.join(ROOT, "lsmdb_amd", "build")
+        lib, flavor = LIB.replace("liblsmgpu.so", "liblsmgpu_stamps.so"), "stamps"
+    if not force and not _stale(lib, deps):
+        return lib
+    objdir = os.path.join(ROOT, "lsmdb_amd", "build", flavor)
     os.makedirs(objdir, exist_ok=True)
+    tag = f".{os.getpid()}.tmp"
     jobs, objs = [], []
     for s in SOURCES:
         obj = os.path.join(objdir, os.path.splitext(s)[0] + ".o")
         objs.append(obj)
-        cmd = flags + ["-c", "-o", obj, os.path.join(CSRC, s)]
+        cmd = flags + ["-c", "-o", obj + tag, os.path.join(CSRC, s)]
         if verbose:
             print("[build]", " ".join(cmd), file=sys.stderr)
         jobs.append(subprocess.Popen(cmd, cwd=CSRC))
-    if any(j.wait() != 0 for j in jobs):
-        raise subprocess.CalledProcessError(1, "hipcc")
-    cmd = flags + ["-shared", "-o", lib] + objs
+    codes = [j.wait() for j in jobs]  # every job finishes before any error is raised
+    if any(codes):
+        for o in objs:
+            if os.path.exists(o + tag):
+                os.remove(o + tag)
+        raise subprocess.CalledProcessError(max(codes), "hipcc")
+    for o in objs:
+        os.replace(o + tag, o)
+    cmd = flags + ["-shared", "-o", lib + tag] + objs
     if verbose:
         print("[build]", " ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=CSRC)
-    return LIB
+    os.replace(lib + tag, lib)
+    return lib
 
 
 def build_oracle(verbose: bool = True) -> str:

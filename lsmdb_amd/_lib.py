@@ -27,6 +27,7 @@ ERR_TOO_LARGE = 7
 ERR_INTERNAL = 8
 ERR_NO_DEVICE = 9
 ERR_CORRUPT = 10
+ERR_HOST_PINNED = 11
 
 BLK_OK = 0
 BLK_VALUE_OVERFLOW = 1
@@ -249,13 +250,15 @@ def _load() -> ctypes.CDLL:
     lib.lsmgpu_compact_tables.restype = c_int
     lib.lsmgpu_compact_result.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p, c_uint64]
     lib.lsmgpu_compact_result.restype = c_int
+    lib.lsmgpu_stream_probe_async.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_uint64,
+                                              c_uint32]
+    lib.lsmgpu_stream_probe_async.restype = c_int
+    if os.environ.get("LSMGPU_LIB_VARIANT") and not hasattr(lib, "lsmgpu_host_register"):
+        return lib  # diagnostics: an earlier round's build (same-box A/B of its kernels)
     lib.lsmgpu_host_register.argtypes = [c_void_p, c_void_p, c_uint64]
     lib.lsmgpu_host_register.restype = c_int
     lib.lsmgpu_host_unregister.argtypes = [c_void_p, c_void_p]
     lib.lsmgpu_host_unregister.restype = c_int
-    lib.lsmgpu_stream_probe_async.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_uint64,
-                                              c_uint32]
-    lib.lsmgpu_stream_probe_async.restype = c_int
     return lib
 
 

@@ -10,10 +10,14 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <shared_mutex>
 #include <vector>
+
+#include <unistd.h>
 
 #include "../../include/lsmgpu.h"
 #include "kernels.hpp"
+#include "pin_registry.hpp"
 
 using namespace lsmgpu;
 
@@ -45,6 +49,44 @@ struct DevBuf {
 inline uint32_t rd_be32(const uint8_t* b) {
   return ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
 }
+
+// the process's page-locked segments (lsmgpu_host_register; pin_registry.hpp)
+PinRegistry& pins() {
+  static PinRegistry r((uintptr_t)sysconf(_SC_PAGESIZE));
+  return r;
+}
+
+// hipMemcpyAsync between HBM and a host range, cut where pinned segments begin and end: HIP serves
+// a copy from the registration its first byte lies in and rejects one that runs past that
+// registration's end (a buffer whose edge pages another caller pinned, or a neighbour's).  Every
+// host copy of the library goes through here.
+hipError_t hcopy(void* dst, const void* src, uint64_t n, hipMemcpyKind kind, hipStream_t s) {
+  if (!n) return hipSuccess;
+  const bool h2d = kind == hipMemcpyHostToDevice;
+  const uintptr_t h = (uintptr_t)(h2d ? src : dst);
+  std::vector<PinRegistry::Range> pc;
+  // shared: copies run concurrently; a re-cut of segments (unregister) waits for them and keeps
+  // new ones out until the re-pin is done
+  std::shared_lock<std::shared_mutex> g(pins().mu());
+  pins().pieces(h, n, &pc);
+  for (const auto& r : pc) {
+    const uint64_t o = r.first - h;
+    hipError_t e = hipMemcpyAsync(static_cast<uint8_t*>(dst) + o, static_cast<const uint8_t*>(src) + o,
+                                  r.second - r.first, kind, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+// Synchronizes the given streams when the scope ends, on every return path: a call that returns
+// (an error included) never leaves DMA into or out of the caller's host buffers in flight.
+struct SyncOnExit {
+  hipStream_t s[3] = {nullptr, nullptr, nullptr};
+  ~SyncOnExit() {
+    for (hipStream_t q : s)
+      if (q) (void)hipStreamSynchronize(q);
+  }
+};
 
 }  // namespace
 
@@ -117,6 +159,7 @@ const char* lsmgpu_strerror(int code) {
     case LSMGPU_ERR_INTERNAL: return "device look-back did not converge";
     case LSMGPU_ERR_NO_DEVICE: return "no HIP device";
     case LSMGPU_ERR_CORRUPT: return "corrupt input table (a block the iterator cannot walk)";
+    case LSMGPU_ERR_HOST_PINNED: return "host memory already page-locked outside the library";
     default: return "unknown error";
   }
 }
@@ -150,7 +193,9 @@ int lsmgpu_open(int device, lsmgpu_ctx** out) {
 void lsmgpu_close(lsmgpu_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+  // nothing may still run on the ctx's streams when their buffers and events go away
+  for (hipStream_t q : {c->own_stream, c->stream, c->s_in, c->s_out})
+    if (q) (void)hipStreamSynchronize(q);
   DevBuf* bufs[] = {&c->lb, &c->result, &c->flags, &c->scan_tmp, &c->wsc,
                     &c->open_tmp, &c->merge_tmp, &c->s_data,
                     &c->s_off, &c->s_len, &c->s_kd, &c->s_ke, &c->s_vd, &c->s_ve, &c->s_view,
@@ -167,8 +212,6 @@ void lsmgpu_close(lsmgpu_ctx* c) {
     for (hipEvent_t* e : {&sl.in_done, &sl.dec_done, &sl.out_done})
       if (*e) (void)hipEventDestroy(*e);
   }
-  if (c->s_in) (void)hipStreamSynchronize(c->s_in);
-  if (c->s_out) (void)hipStreamSynchronize(c->s_out);
   if (c->s_in) (void)hipStreamDestroy(c->s_in);
   if (c->s_out) (void)hipStreamDestroy(c->s_out);
   if (c->h_chunk_res) (void)hipHostFree(c->h_chunk_res);
@@ -418,26 +461,82 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
 }
 
 int lsmgpu_host_register(lsmgpu_ctx* c, void* p, uint64_t bytes) {
-  if (!c || !p || !bytes) return LSMGPU_ERR_ARG;
+  if (!c || !p || !bytes || (uintptr_t)p + bytes < (uintptr_t)p) return LSMGPU_ERR_ARG;
   HIPC(hipSetDevice(c->device));
-  // read-only first (an mmap'd .sst is PROT_READ), then read-write memory
-  hipError_t e = hipHostRegister(p, bytes, hipHostRegisterPortable | hipHostRegisterReadOnly);
-  if (e != hipSuccess && e != hipErrorHostMemoryAlreadyRegistered) {
-    (void)hipGetLastError();
-    e = hipHostRegister(p, bytes, hipHostRegisterPortable);
+  PinRegistry& R = pins();
+  std::unique_lock<std::shared_mutex> g(R.mu());
+  // pin only the pages no segment covers yet, each run as a segment of its own
+  const std::vector<PinRegistry::Range> gaps = R.gaps((uintptr_t)p, bytes);
+  std::vector<PinRegistry::Range> made;
+  int rc = LSMGPU_OK;
+  for (const auto& gp : gaps) {
+    void* q = reinterpret_cast<void*>(gp.first);
+    const size_t n = gp.second - gp.first;
+    hipError_t e = hipHostRegister(q, n, hipHostRegisterPortable);
+    if (e != hipSuccess && e != hipErrorHostMemoryAlreadyRegistered) {
+      (void)hipGetLastError();  // a PROT_READ mapping (an mmap'd .sst) pins read-only
+      e = hipHostRegister(q, n, hipHostRegisterPortable | hipHostRegisterReadOnly);
+    }
+    if (e != hipSuccess) {
+      report_hip_error("hipHostRegister", e, __LINE__);
+      (void)hipGetLastError();
+      // pinned outside this library (hipHostMalloc, the caller's own hipHostRegister): those
+      // pages are not ours to pin or unpin, and nothing of the range is registered here
+      rc = e == hipErrorHostMemoryAlreadyRegistered ? LSMGPU_ERR_HOST_PINNED : LSMGPU_ERR_HIP;
+      break;
+    }
+    made.push_back(gp);
   }
-  if (e == hipErrorHostMemoryAlreadyRegistered) {
+  if (rc != LSMGPU_OK) {
+    for (const auto& m : made) (void)hipHostUnregister(reinterpret_cast<void*>(m.first));
     (void)hipGetLastError();
-    return LSMGPU_OK;
+    return rc;
   }
-  return e == hipSuccess ? LSMGPU_OK : LSMGPU_ERR_HIP;
+  R.add((uintptr_t)p, bytes, made);
+  return LSMGPU_OK;
 }
 
 int lsmgpu_host_unregister(lsmgpu_ctx* c, void* p) {
   if (!c || !p) return LSMGPU_ERR_ARG;
   HIPC(hipSetDevice(c->device));
-  HIPC(hipHostUnregister(p));
-  return LSMGPU_OK;
+  PinRegistry& R = pins();
+  std::unique_lock<std::shared_mutex> g(R.mu());
+  std::vector<PinRegistry::Range> unpin, repin;
+  bool recut = false;
+  if (!R.remove((uintptr_t)p, &unpin, &repin, &recut)) return LSMGPU_ERR_ARG;  // not registered here
+  if (recut) {
+    // a segment other ranges still use in part is unpinned and its covered runs pinned again:
+    // drain every device first (no copy from those pages in flight; new copies wait on the lock)
+    int ndev = 0;
+    (void)hipGetDeviceCount(&ndev);
+    for (int d = 0; d < ndev; d++)
+      if (hipSetDevice(d) == hipSuccess) (void)hipDeviceSynchronize();
+    (void)hipSetDevice(c->device);
+  }
+  int rc = LSMGPU_OK;
+  for (const auto& r : unpin) {
+    hipError_t e = hipHostUnregister(reinterpret_cast<void*>(r.first));
+    if (e != hipSuccess) {
+      report_hip_error("hipHostUnregister", e, __LINE__);
+      (void)hipGetLastError();
+      rc = LSMGPU_ERR_HIP;
+    }
+  }
+  for (const auto& r : repin) {
+    void* q = reinterpret_cast<void*>(r.first);
+    hipError_t e = hipHostRegister(q, r.second - r.first, hipHostRegisterPortable);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      e = hipHostRegister(q, r.second - r.first, hipHostRegisterPortable | hipHostRegisterReadOnly);
+    }
+    if (e != hipSuccess) {  // those pages stay unpinned: copies from them are staged, still correct
+      report_hip_error("hipHostRegister (re-cut)", e, __LINE__);
+      (void)hipGetLastError();
+      R.drop(r);
+      rc = LSMGPU_ERR_HIP;
+    }
+  }
+  return rc;
 }
 
 }  // extern "C"
@@ -513,16 +612,17 @@ int decode_host_pipelined(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
     for (hipEvent_t* e : {&sl.in_done, &sl.dec_done, &sl.out_done})
       if (!*e) HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
   }
+  // every return below (errors included) first drains the three streams: no copy into the
+  // caller's arrays outlives the call
+  SyncOnExit drain_all;
+  drain_all.s[0] = c->s_in;
+  drain_all.s[1] = c->stream;
+  drain_all.s[2] = c->s_out;
   // running totals of the chunks already placed
   uint64_t E = 0, KB = 0, VB = 0, nbad = 0;
   int64_t first_bad = -1;
   bool fits = true;
   std::vector<uint8_t> slot_used(lsmgpu_ctx::kSlots, 0);
-  auto drain = [&]() {
-    (void)hipStreamSynchronize(c->s_in);
-    (void)hipStreamSynchronize(c->stream);
-    (void)hipStreamSynchronize(c->s_out);
-  };
   for (uint64_t i = 0; i <= nch; i++) {
     if (i < nch) {  // chunk i: copy in, decode
       auto& sl = c->slot[i % lsmgpu_ctx::kSlots];
@@ -530,9 +630,9 @@ int decode_host_pipelined(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
       const uint64_t a = blk_off[b0] & ~127ull, e = (uint64_t)blk_off[cb[i + 1] - 1] + blk_len[cb[i + 1] - 1];
       if (slot_used[i % lsmgpu_ctx::kSlots]) HIPC(hipStreamWaitEvent(c->s_in, sl.out_done, 0));
       slot_used[i % lsmgpu_ctx::kSlots] = 1;
-      HIPC(hipMemcpyAsync(sl.data.p, data + a, e - a, hipMemcpyHostToDevice, c->s_in));
-      HIPC(hipMemcpyAsync(sl.off.p, blk_off + b0, nb * 4, hipMemcpyHostToDevice, c->s_in));
-      HIPC(hipMemcpyAsync(sl.len.p, blk_len + b0, nb * 4, hipMemcpyHostToDevice, c->s_in));
+      HIPC(hcopy(sl.data.p, data + a, e - a, hipMemcpyHostToDevice, c->s_in));
+      HIPC(hcopy(sl.off.p, blk_off + b0, nb * 4, hipMemcpyHostToDevice, c->s_in));
+      HIPC(hcopy(sl.len.p, blk_len + b0, nb * 4, hipMemcpyHostToDevice, c->s_in));
       HIPC(hipEventRecord(sl.in_done, c->s_in));
       HIPC(hipStreamWaitEvent(c->stream, sl.in_done, 0));
       lsmgpu_decoded d{};
@@ -555,10 +655,7 @@ int decode_host_pipelined(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
       int rc = lsmgpu_decode_blocks_async(c, sl.data.as<uint8_t>() - a, e,
                                           sl.off.as<uint32_t>(), sl.len.as<uint32_t>(), nb, ml,
                                           mode, &d, sl.res.as<uint64_t>());
-      if (rc != LSMGPU_OK) {
-        drain();
-        return rc;
-      }
+      if (rc != LSMGPU_OK) return rc;
       HIPC(hipMemcpyAsync(c->h_chunk_res + 8 * (i % lsmgpu_ctx::kSlots), sl.res.p, 64,
                           hipMemcpyDeviceToHost, c->stream));
       HIPC(hipEventRecord(sl.dec_done, c->stream));
@@ -570,14 +667,8 @@ int decode_host_pipelined(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
     HIPC(hipEventSynchronize(sl.dec_done));
     const uint64_t* r = c->h_chunk_res + 8 * (j % lsmgpu_ctx::kSlots);
     const uint64_t n = r[0], kb = r[1], vb = r[2], fb = r[3], bad = r[4], fl = r[5];
-    if (fl & 2) {
-      drain();
-      return LSMGPU_ERR_INTERNAL;
-    }
-    if (fl & 1) {  // a chunk outgrew its slot (expanding prefix-compressed keys)
-      drain();
-      return kNotPipelined;
-    }
+    if (fl & 2) return LSMGPU_ERR_INTERNAL;
+    if (fl & 1) return kNotPipelined;  // a chunk outgrew its slot (expanding prefix-compressed keys)
     if (fb && first_bad < 0) first_bad = (int64_t)(b0 + nb - fb);
     nbad += bad;
     fits = fits && E + n <= out->ent_cap && E + n <= 0xffffffffull &&
@@ -596,7 +687,7 @@ int decode_host_pipelined(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
     }
     auto back = [&](void* hp, const void* dp, uint64_t bytes) -> hipError_t {
       if (!hp || !bytes) return hipSuccess;
-      return hipMemcpyAsync(hp, dp, bytes, hipMemcpyDeviceToHost, c->s_out);
+      return hcopy(hp, dp, bytes, hipMemcpyDeviceToHost, c->s_out);
     };
     if (fits) {
       if (mat) {
@@ -643,11 +734,13 @@ int lsmgpu_decode_blocks(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
     const int prc = decode_host_pipelined(c, data, data_len, blk_off, blk_len, nblk, mode, out, max_len);
     if (prc != kNotPipelined) return prc;
   }
+  SyncOnExit sync_exit;  // no DMA into the caller's arrays outlives the call, errors included
+  sync_exit.s[0] = c->stream;
   HIPC(c->s_off.ensure((nblk + 1) * 4));
   HIPC(c->s_len.ensure((nblk + 1) * 4));
   if (nblk) {
-    HIPC(hipMemcpyAsync(c->s_off.p, blk_off, nblk * 4, hipMemcpyHostToDevice, c->stream));
-    HIPC(hipMemcpyAsync(c->s_len.p, blk_len, nblk * 4, hipMemcpyHostToDevice, c->stream));
+    HIPC(hcopy(c->s_off.p, blk_off, nblk * 4, hipMemcpyHostToDevice, c->stream));
+    HIPC(hcopy(c->s_len.p, blk_len, nblk * 4, hipMemcpyHostToDevice, c->stream));
   }
   lsmgpu_decoded d = *out;
   // every output pointer NULL = a size query: the blocks are walked, n_entries / key_bytes /
@@ -661,7 +754,7 @@ int lsmgpu_decode_blocks(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
   const uint8_t* d_data = data;
   if (!data_on_device) {  // stage host buffers through HBM
     HIPC(c->s_data.ensure(data_len + 16));
-    if (data_len) HIPC(hipMemcpyAsync(c->s_data.p, data, data_len, hipMemcpyHostToDevice, c->stream));
+    if (data_len) HIPC(hcopy(c->s_data.p, data, data_len, hipMemcpyHostToDevice, c->stream));
     d_data = c->s_data.as<uint8_t>();
     auto stage = [&](DevBuf& b, void* hp, uint64_t bytes) -> void* {
       if (!hp) return nullptr;
@@ -695,7 +788,7 @@ int lsmgpu_decode_blocks(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
   if (!data_on_device) {
     auto back = [&](void* hp, const void* dp, uint64_t bytes) -> hipError_t {
       if (!hp || !bytes) return hipSuccess;
-      return hipMemcpyAsync(hp, dp, bytes, hipMemcpyDeviceToHost, c->stream);
+      return hcopy(hp, dp, bytes, hipMemcpyDeviceToHost, c->stream);
     };
     const bool fits = !(flags & 1);
     uint64_t ne = fits ? out->n_entries : 0;
@@ -795,6 +888,8 @@ int lsmgpu_encode_blocks(lsmgpu_ctx* c, const uint8_t* keys, const uint32_t* key
   if (query && on_device && !c) return LSMGPU_ERR_ARG;
   if (epb == 0 && block_bytes == 0) return LSMGPU_ERR_ARG;
   if (c) HIPC(hipSetDevice(c->device));
+  SyncOnExit sync_exit;
+  if (c) sync_exit.s[0] = c->stream;
   // host copies of the offset columns (needed for totals and the byte-target plan)
   std::vector<uint32_t> hk, hv;
   const uint32_t* hke = key_end;
@@ -802,8 +897,8 @@ int lsmgpu_encode_blocks(lsmgpu_ctx* c, const uint8_t* keys, const uint32_t* key
   if (on_device && n) {
     hk.resize(n);
     hv.resize(n);
-    HIPC(hipMemcpyAsync(hk.data(), key_end, n * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPC(hipMemcpyAsync(hv.data(), vs_end, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hcopy(hk.data(), key_end, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hcopy(hv.data(), vs_end, n * 4, hipMemcpyDeviceToHost, c->stream));
     HIPC(hipStreamSynchronize(c->stream));
     hke = hk.data();
     hve = hv.data();
@@ -846,11 +941,11 @@ int lsmgpu_encode_blocks(lsmgpu_ctx* c, const uint8_t* keys, const uint32_t* key
     HIPC(c->s_c.ensure(vs_total + 16));
     HIPC(c->s_d.ensure(n * 4 + 16));
     HIPC(c->s_kd.ensure(total + 16));
-    if (key_total) HIPC(hipMemcpyAsync(c->s_a.p, keys, key_total, hipMemcpyHostToDevice, c->stream));
-    if (vs_total) HIPC(hipMemcpyAsync(c->s_c.p, vs, vs_total, hipMemcpyHostToDevice, c->stream));
+    if (key_total) HIPC(hcopy(c->s_a.p, keys, key_total, hipMemcpyHostToDevice, c->stream));
+    if (vs_total) HIPC(hcopy(c->s_c.p, vs, vs_total, hipMemcpyHostToDevice, c->stream));
     if (n) {
-      HIPC(hipMemcpyAsync(c->s_b.p, key_end, n * 4, hipMemcpyHostToDevice, c->stream));
-      HIPC(hipMemcpyAsync(c->s_d.p, vs_end, n * 4, hipMemcpyHostToDevice, c->stream));
+      HIPC(hcopy(c->s_b.p, key_end, n * 4, hipMemcpyHostToDevice, c->stream));
+      HIPC(hcopy(c->s_d.p, vs_end, n * 4, hipMemcpyHostToDevice, c->stream));
     }
     dk = c->s_a.as<uint8_t>();
     dke = c->s_b.as<uint32_t>();
@@ -861,7 +956,7 @@ int lsmgpu_encode_blocks(lsmgpu_ctx* c, const uint8_t* keys, const uint32_t* key
   const uint32_t* dplan = nullptr;
   if (explicit_plan) {
     HIPC(c->s_bf.ensure((nb + 1) * 4));
-    HIPC(hipMemcpyAsync(c->s_bf.p, plan.data(), (nb + 1) * 4, hipMemcpyHostToDevice, c->stream));
+    HIPC(hcopy(c->s_bf.p, plan.data(), (nb + 1) * 4, hipMemcpyHostToDevice, c->stream));
     dplan = c->s_bf.as<uint32_t>();
   }
   HIPC(hipMemsetAsync(c->flags.p, 0, 16, c->stream));
@@ -869,8 +964,8 @@ int lsmgpu_encode_blocks(lsmgpu_ctx* c, const uint8_t* keys, const uint32_t* key
                                       dout, total, c->flags.as<uint32_t>());
   if (rc != LSMGPU_OK) return rc;
   uint32_t hflags[4] = {0, 0, 0, 0};
-  HIPC(hipMemcpyAsync(hflags, c->flags.p, 16, hipMemcpyDeviceToHost, c->stream));
-  if (!on_device) HIPC(hipMemcpyAsync(out, dout, total, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hcopy(hflags, c->flags.p, 16, hipMemcpyDeviceToHost, c->stream));
+  if (!on_device) HIPC(hcopy(out, dout, total, hipMemcpyDeviceToHost, c->stream));
   HIPC(hipStreamSynchronize(c->stream));
   if (hflags[0] & 1) return LSMGPU_ERR_KEY_LEN;
   if (hflags[0] & 2) return LSMGPU_ERR_VALUE_LEN;
@@ -878,7 +973,8 @@ int lsmgpu_encode_blocks(lsmgpu_ctx* c, const uint8_t* keys, const uint32_t* key
     if (nb > restarts_cap) return LSMGPU_ERR_CAPACITY;
     std::vector<uint8_t> idx(4 * nb);
     if (on_device) {
-      HIPC(hipMemcpy(idx.data(), out + dl, 4 * nb, hipMemcpyDeviceToHost));
+      HIPC(hcopy(idx.data(), out + dl, 4 * nb, hipMemcpyDeviceToHost, c->stream));
+      HIPC(hipStreamSynchronize(c->stream));
     } else {
       std::memcpy(idx.data(), out + dl, 4 * nb);
     }
@@ -897,10 +993,12 @@ int lsmgpu_encode_values(lsmgpu_ctx* c, const uint8_t* meta, const uint8_t* user
   if (n == 0) return LSMGPU_OK;
   if (!meta || !user_meta || !expires_at || !value_end || !vs || !vs_end) return LSMGPU_ERR_ARG;
   HIPC(hipSetDevice(c->device));
+  SyncOnExit sync_exit;
+  sync_exit.s[0] = c->stream;
   uint64_t vtotal = 0;
   if (on_device) {
     uint32_t last = 0;
-    HIPC(hipMemcpyAsync(&last, value_end + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hcopy(&last, value_end + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
     HIPC(hipStreamSynchronize(c->stream));
     vtotal = last;
   } else {
@@ -919,11 +1017,11 @@ int lsmgpu_encode_values(lsmgpu_ctx* c, const uint8_t* meta, const uint8_t* user
     HIPC(c->s_d.ensure(n * 4 + 16));
     HIPC(c->s_ve.ensure(n * 4 + 16));
     uint8_t* dm = c->s_a.as<uint8_t>();
-    HIPC(hipMemcpyAsync(dm, meta, n, hipMemcpyHostToDevice, c->stream));
-    HIPC(hipMemcpyAsync(dm + n, user_meta, n, hipMemcpyHostToDevice, c->stream));
-    HIPC(hipMemcpyAsync(c->s_b.p, expires_at, n * 8, hipMemcpyHostToDevice, c->stream));
-    if (vtotal) HIPC(hipMemcpyAsync(c->s_c.p, values, vtotal, hipMemcpyHostToDevice, c->stream));
-    HIPC(hipMemcpyAsync(c->s_d.p, value_end, n * 4, hipMemcpyHostToDevice, c->stream));
+    HIPC(hcopy(dm, meta, n, hipMemcpyHostToDevice, c->stream));
+    HIPC(hcopy(dm + n, user_meta, n, hipMemcpyHostToDevice, c->stream));
+    HIPC(hcopy(c->s_b.p, expires_at, n * 8, hipMemcpyHostToDevice, c->stream));
+    if (vtotal) HIPC(hcopy(c->s_c.p, values, vtotal, hipMemcpyHostToDevice, c->stream));
+    HIPC(hcopy(c->s_d.p, value_end, n * 4, hipMemcpyHostToDevice, c->stream));
     p.meta = dm; p.user_meta = dm + n; p.expires_at = c->s_b.as<uint64_t>();
     p.values = c->s_c.as<uint8_t>(); p.value_end = c->s_d.as<uint32_t>();
     p.vs_end = c->s_ve.as<uint32_t>();
@@ -941,7 +1039,7 @@ int lsmgpu_encode_values(lsmgpu_ctx* c, const uint8_t* meta, const uint8_t* user
                                rocprim::plus<uint32_t>(), c->stream));
   p.vs_end = final_end;
   uint32_t total = 0;
-  HIPC(hipMemcpyAsync(&total, p.vs_end + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hcopy(&total, p.vs_end + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
   HIPC(hipStreamSynchronize(c->stream));
   *vs_len = total;
   if (total > vs_cap) return LSMGPU_ERR_CAPACITY;
@@ -951,8 +1049,8 @@ int lsmgpu_encode_values(lsmgpu_ctx* c, const uint8_t* meta, const uint8_t* user
   }
   HIPC(launch_values_write(p, c->stream));
   if (!on_device) {
-    HIPC(hipMemcpyAsync(vs, p.vs, total, hipMemcpyDeviceToHost, c->stream));
-    HIPC(hipMemcpyAsync(vs_end, p.vs_end, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hcopy(vs, p.vs, total, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hcopy(vs_end, p.vs_end, n * 4, hipMemcpyDeviceToHost, c->stream));
   }
   HIPC(hipStreamSynchronize(c->stream));
   return LSMGPU_OK;
@@ -1390,6 +1488,8 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
   for (uint32_t r = 0; r < nruns; r++)
     if (run_first[r + 1] < run_first[r]) return LSMGPU_ERR_ARG;
   HIPC(hipSetDevice(c->device));
+  SyncOnExit sync_exit;
+  sync_exit.s[0] = c->stream;
   // 1. every table's tail (Table.readIndex, table.go:177-215) -> one block list over the
   //    concatenated data regions; run r starts at block rblk[r]
   std::vector<uint32_t> off, len;
@@ -1421,7 +1521,7 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
   HIPC(c->cp_data.ensure(data_len + 64));
   for (uint32_t t = 0; t < ntables; t++)
     if (base[t + 1] > base[t])
-      HIPC(hipMemcpyAsync(c->cp_data.as<uint8_t>() + base[t], ssts[t], base[t + 1] - base[t],
+      HIPC(hcopy(c->cp_data.as<uint8_t>() + base[t], ssts[t], base[t + 1] - base[t],
                           hipMemcpyHostToDevice, c->stream));
   HIPC(c->cp_res.ensure(64));
   uint64_t* d_res = c->cp_res.as<uint64_t>();
@@ -1433,8 +1533,8 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
     HIPC(c->cp_off.ensure(nb * 4 + 4));
     HIPC(c->cp_len.ensure(nb * 4 + 4));
     if (nb) {
-      HIPC(hipMemcpyAsync(c->cp_off.p, o.data(), nb * 4, hipMemcpyHostToDevice, c->stream));
-      HIPC(hipMemcpyAsync(c->cp_len.p, l.data(), nb * 4, hipMemcpyHostToDevice, c->stream));
+      HIPC(hcopy(c->cp_off.p, o.data(), nb * 4, hipMemcpyHostToDevice, c->stream));
+      HIPC(hcopy(c->cp_len.p, l.data(), nb * 4, hipMemcpyHostToDevice, c->stream));
     }
     uint64_t kcap = std::max<uint64_t>(data_len, 16), vcap = kcap, ecap = data_len / 10 + 1;
     for (int attempt = 0;; attempt++) {  // plen > 0 blocks can expand keys: resize once
@@ -1458,7 +1558,7 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
                                           c->cp_off.as<uint32_t>(), c->cp_len.as<uint32_t>(), nb,
                                           max_len, LSMGPU_MODE_MATERIALIZE, &d, d_res);
       if (rc != LSMGPU_OK) return rc;
-      HIPC(hipMemcpyAsync(r, d_res, 64, hipMemcpyDeviceToHost, c->stream));
+      HIPC(hcopy(r, d_res, 64, hipMemcpyDeviceToHost, c->stream));
       HIPC(hipStreamSynchronize(c->stream));
       if (r[5] & 2) return LSMGPU_ERR_INTERNAL;
       if (!(r[5] & 1)) break;
@@ -1469,8 +1569,8 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
     }
     bf.assign(nb + 1, 0);
     bs.assign(nb + 1, 0);
-    HIPC(hipMemcpyAsync(bf.data(), c->cp_bf.p, (nb + 1) * 4, hipMemcpyDeviceToHost, c->stream));
-    if (nb) HIPC(hipMemcpyAsync(bs.data(), c->cp_bs.p, nb * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hcopy(bf.data(), c->cp_bf.p, (nb + 1) * 4, hipMemcpyDeviceToHost, c->stream));
+    if (nb) HIPC(hcopy(bs.data(), c->cp_bs.p, nb * 4, hipMemcpyDeviceToHost, c->stream));
     HIPC(hipStreamSynchronize(c->stream));
     return LSMGPU_OK;
   };
@@ -1547,7 +1647,7 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
     return LSMGPU_OK;
   }
   HIPC(c->cp_rf.ensure((nruns + 1) * 4));
-  HIPC(hipMemcpyAsync(c->cp_rf.p, rf.data(), (nruns + 1) * 4, hipMemcpyHostToDevice, c->stream));
+  HIPC(hcopy(c->cp_rf.p, rf.data(), (nruns + 1) * 4, hipMemcpyHostToDevice, c->stream));
   // 4. MergeIterator (y/iterator.go:74-202): lower run index wins ties, duplicates dropped
   // the merge writes the merged order (source index + end offsets), not the bytes: the
   // encoder reads each entry's bytes from the decoded tables, the one copy builder.Add makes
@@ -1561,7 +1661,7 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
   int rc = lsmgpu_merge_runs_async(c, &runs, &mo, d_res);
   if (rc != LSMGPU_OK) return rc;
   uint64_t m[8];
-  HIPC(hipMemcpyAsync(m, d_res, 64, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hcopy(m, d_res, 64, hipMemcpyDeviceToHost, c->stream));
   HIPC(hipStreamSynchronize(c->stream));
   if (m[3] & LSMGPU_MERGE_TIMEOUT) return LSMGPU_ERR_INTERNAL;
   if (m[3] & LSMGPU_MERGE_KEY_LEN) return LSMGPU_ERR_KEY_LEN;
@@ -1581,7 +1681,7 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
                                     c->cp_tf.as<uint32_t>(), c->cp_tb.as<uint32_t>(),
                                     c->cp_to.as<uint64_t>(), (uint32_t)tcap, d_res);
     if (rc != LSMGPU_OK) return rc;
-    HIPC(hipMemcpyAsync(cut, d_res, 64, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hcopy(cut, d_res, 64, hipMemcpyDeviceToHost, c->stream));
     HIPC(hipStreamSynchronize(c->stream));
     if (!cut[3]) break;
     if (attempt || tcap >= mn) return LSMGPU_ERR_INTERNAL;
@@ -1604,8 +1704,8 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
   if (rc != LSMGPU_OK) return rc;
   std::vector<uint32_t> tf(nt + 1);
   c->cp_tbl_out.assign(nt + 1, 0);
-  HIPC(hipMemcpyAsync(tf.data(), c->cp_tf.p, (nt + 1) * 4, hipMemcpyDeviceToHost, c->stream));
-  HIPC(hipMemcpyAsync(c->cp_tbl_out.data(), c->cp_to.p, (nt + 1) * 8, hipMemcpyDeviceToHost,
+  HIPC(hcopy(tf.data(), c->cp_tf.p, (nt + 1) * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hcopy(c->cp_tbl_out.data(), c->cp_to.p, (nt + 1) * 8, hipMemcpyDeviceToHost,
                       c->stream));
   HIPC(hipStreamSynchronize(c->stream));
   if (bloom) {
@@ -1629,7 +1729,7 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
     if (rc != LSMGPU_OK) return compact_fail(c, rc);
   }
   uint32_t fl[4];
-  HIPC(hipMemcpyAsync(fl, c->cp_flags.p, 16, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hcopy(fl, c->cp_flags.p, 16, hipMemcpyDeviceToHost, c->stream));
   HIPC(hipStreamSynchronize(c->stream));
   if ((fl[0] & 1) || (fl[1] & 1)) return LSMGPU_ERR_KEY_LEN;
   if (fl[0] & 2) return LSMGPU_ERR_VALUE_LEN;
@@ -1647,8 +1747,10 @@ extern "C" int lsmgpu_compact_result(lsmgpu_ctx* c, uint8_t* out, uint64_t out_c
   if (out_cap < c->cp_bytes || tbl_cap < nt + 1) return LSMGPU_ERR_CAPACITY;
   if ((c->cp_bytes && !out) || !tbl_off) return LSMGPU_ERR_ARG;
   HIPC(hipSetDevice(c->device));
+  SyncOnExit sync_exit;
+  sync_exit.s[0] = c->stream;
   if (c->cp_bytes)
-    HIPC(hipMemcpyAsync(out, c->cp_out.p, c->cp_bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hcopy(out, c->cp_out.p, c->cp_bytes, hipMemcpyDeviceToHost, c->stream));
   HIPC(hipStreamSynchronize(c->stream));
   std::memcpy(tbl_off, c->cp_tbl_out.data(), (nt + 1) * 8);
   return LSMGPU_OK;

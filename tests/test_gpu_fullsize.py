@@ -58,6 +58,45 @@ def test_c2_full_gib_round_trip(codec):
     assert torch.equal(sst[kpos + klen], w["d_vs"][ve - vlen])
 
 
+def test_c2_full_gib_repeated_view_and_materialize(codec):
+    """The live walk's shared prefix machinery under repetition at 2^30 B: 1,041 walk tiles for
+    1,024 resident workgroup slots (more workgroups than fit at once), the ticket counter reset
+    by the last ticket of each launch, epoch-tagged tile records never cleared between launches
+    and the decoupled look-back.  40 decodes back to back alternate view-only (the fused view
+    epilogue) and materialize (walk + copy); every one must give the block plan as blk_first,
+    no error flag, and the same view records / end offsets as the first.  (Round 4's removed
+    one-pass kernel produced a wrong block index once and shared the ticket / tag / look-back
+    primitives -- DESIGN section 5.)"""
+    import torch
+    import bench
+    from lsmdb_amd.codec import MODE_MATERIALIZE, MODE_VIEW
+    dev = torch.device("cuda", codec.device)
+    torch.cuda.set_device(dev)
+    w = bench.build_device_sst(codec, torch, dev, 2, 1 << 30, 0)
+    assert (w["nblocks"] + 255) // 256 > 4 * 256  # more walk tiles than resident workgroups
+    vb = codec.alloc_decode(w["data_len"], 0, w["nblocks"], MODE_VIEW, ent_cap=w["n"])
+    mb = codec.alloc_decode(w["data_len"], w["data_len"], w["nblocks"], MODE_MATERIALIZE, ent_cap=w["n"])
+    plan = w["d_plan"]
+    first_view = None
+    for i in range(40):
+        view = i % 2 == 0
+        b = vb if view else mb
+        codec.decode_device_async(w["d_sst"], w["d_off"], w["d_len"], w["max_len"],
+                                  MODE_VIEW if view else MODE_MATERIALIZE, b, data_len=w["data_len"])
+        codec.synchronize()
+        r = b.result.cpu().numpy()
+        assert int(r[0]) == w["n"] and r[4] == 0 and r[5] == 0, (i, r)
+        assert torch.equal(b.blk_first[: w["nblocks"] + 1], plan), i
+        if view:
+            if first_view is None:
+                first_view = b.view[: w["n"]].clone()
+            else:
+                assert torch.equal(b.view[: w["n"]], first_view), i
+        else:
+            assert torch.equal(b.key_end[: w["n"]], w["d_ke"]) and torch.equal(b.val_end[: w["n"]], w["d_ve"]), i
+    assert torch.equal(mb.key_data[: w["key_total"]], w["d_keys"])
+
+
 def _c4_table(oracle, seed: int, select=None) -> bytes:
     """One 64 MiB ReachedCapacity(64 MiB)-cut table, oracle-built (100 entries per block)."""
     import bench

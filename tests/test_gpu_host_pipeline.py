@@ -5,7 +5,6 @@ sizes of 1-3 MiB (LSMGPU_HOST_CHUNK) cut the test inputs into many chunks, so th
 bases, the block-index and status arrays across chunk borders, the first bad block and the
 capacity rules are all exercised; every output is checked against the oracle.  Unsorted block
 lists and chunks whose prefix-compressed keys outgrow their device slot take the one-shot path."""
-import ctypes
 from ctypes import byref
 
 import numpy as np
@@ -40,43 +39,128 @@ def _mixed(oracle):
 
 @pytest.fixture(scope="module")
 def mixed(oracle):
-    """The mixed input, its oracle decode, and a page-aligned copy of it registered once for the
-    module (lsmgpu_host_register, as the shim pins an mmap): registering one buffer per test
-    re-registers whatever pages the allocator hands back, a pattern the shim never has."""
-    from lsmdb_amd.codec import Codec
     data, off, ln = _mixed(oracle)
-    ref = oracle.decode(data, off, ln)
-    page = 4096
-    raw = np.zeros(len(data) + 2 * page, np.uint8)
-    a = (-raw.ctypes.data) % page
-    pinned = raw[a:a + len(data)]
-    pinned[:] = np.frombuffer(data, np.uint8)
-    reg = Codec(0)
-    reg.host_register(pinned)
-    yield data, off, ln, ref, pinned
-    reg.host_unregister(pinned)
-    reg.close()
-    del raw
+    return data, off, ln, oracle.decode(data, off, ln)
+
+
+def _check(g, ref, m, what):
+    if m == MODE_VIEW:
+        assert g.n_entries == ref.n_entries and np.array_equal(g.view, ref.view), what
+        assert np.array_equal(g.blk_first, ref.blk_first), what
+        assert np.array_equal(g.blk_status, ref.blk_status), what
+        assert g.first_bad_block == ref.first_bad_block and g.n_bad_blocks == ref.n_bad_blocks, what
+    else:
+        if m == MODE_MATERIALIZE:
+            g.view = None
+        _assert_same(g, ref, what)
 
 
 @pytest.mark.parametrize("chunk", ["1048576", "3000000"])
 @pytest.mark.parametrize("mode", ["both", "view", "materialize"])
 def test_host_pipeline_vs_oracle(codec, mixed, monkeypatch, chunk, mode):
+    """Pageable and pinned input, pinned per test (register -> decode -> unregister) on a fresh
+    buffer: the allocator hands back pages of earlier tests' buffers, as compaction's
+    OpenTable / DecrRef cycles do (levels.go:281-298, table/table.go:53-71)."""
     monkeypatch.setenv("LSMGPU_HOST_CHUNK", chunk)
-    data, off, ln, ref, pinned_buf = mixed
+    data, off, ln, ref = mixed
     m = {"both": MODE_MATERIALIZE | MODE_VIEW, "view": MODE_VIEW, "materialize": MODE_MATERIALIZE}[mode]
     for pinned in (False, True):
-        buf = pinned_buf if pinned else np.frombuffer(data, np.uint8).copy()
-        g = codec.decode_host(buf, off, ln, mode=m)
-        if m == MODE_VIEW:
-            assert g.n_entries == ref.n_entries and np.array_equal(g.view, ref.view)
-            assert np.array_equal(g.blk_first, ref.blk_first)
-            assert np.array_equal(g.blk_status, ref.blk_status)
-            assert g.first_bad_block == ref.first_bad_block and g.n_bad_blocks == ref.n_bad_blocks
-        else:
-            if m == MODE_MATERIALIZE:
-                g.view = None
-            _assert_same(g, ref, f"chunk={chunk} pinned={pinned}")
+        buf = np.frombuffer(data, np.uint8).copy()
+        if pinned:
+            codec.host_register(buf)
+        try:
+            g = codec.decode_host(buf, off, ln, mode=m)
+        finally:
+            if pinned:
+                codec.host_unregister(buf)
+        _check(g, ref, m, f"chunk={chunk} pinned={pinned}")
+
+
+def test_host_register_shared_pages(codec, mixed, monkeypatch):
+    """Two non-page-aligned copies of the input in one allocation, 16 B apart (a page shared by
+    both, as Go heap buffers under LoadToRAM share pages, table/table.go:117-123,329-338): both
+    pinned, both decoded, the first unpinned (its segment is re-cut: the second still needs the
+    shared page) and the second decoded again, then unpinned."""
+    monkeypatch.setenv("LSMGPU_HOST_CHUNK", "1048576")
+    data, off, ln, ref = mixed
+    n = len(data)
+    big = np.zeros(2 * n + 8192, np.uint8)
+    a0 = 100 + (-big.ctypes.data) % 4096  # 100 B past a page start
+    a = big[a0:a0 + n]
+    b = big[a0 + n + 16:a0 + 2 * n + 16]
+    a[:] = np.frombuffer(data, np.uint8)
+    b[:] = a
+    codec.host_register(a)
+    codec.host_register(b)
+    _check(codec.decode_host(a, off, ln), ref, 3, "a")
+    _check(codec.decode_host(b, off, ln), ref, 3, "b")
+    codec.host_unregister(a)
+    _check(codec.decode_host(b, off, ln), ref, 3, "b after a unpinned")
+    codec.host_unregister(b)
+    _check(codec.decode_host(a, off, ln), ref, 3, "a unpinned")
+
+
+def test_host_register_cycles_and_nesting(codec, mixed, monkeypatch):
+    """register / unregister / register again at one address; a sub-range registered inside a
+    pinned range (no new pin) and decoded at an unaligned pointer; unregistering in either order;
+    an unknown pointer is LSMGPU_ERR_ARG."""
+    monkeypatch.setenv("LSMGPU_HOST_CHUNK", "1048576")
+    data, off, ln, ref = mixed
+    buf = np.zeros(len(data) + 4096 + 13, np.uint8)
+    sub = buf[13:13 + len(data)]
+    sub[:] = np.frombuffer(data, np.uint8)
+    for _ in range(3):
+        codec.host_register(sub)
+        _check(codec.decode_host(sub, off, ln), ref, 3, "cycle")
+        codec.host_unregister(sub)
+    codec.host_register(buf)
+    codec.host_register(sub)  # nested: every page already pinned
+    _check(codec.decode_host(sub, off, ln), ref, 3, "nested")
+    codec.host_unregister(buf)  # the outer range goes first: sub keeps its pages
+    _check(codec.decode_host(sub, off, ln), ref, 3, "nested, outer unpinned")
+    codec.host_unregister(sub)
+    rc = _lib.lib().lsmgpu_host_unregister(codec._ctx, _ptr(sub))
+    assert rc == _lib.ERR_ARG
+
+
+def test_host_register_readonly_mmap(codec, oracle, tmp_path, monkeypatch):
+    """A real .sst file mmap'd read-only (MemoryMap mode, table/table.go:88-144, y/mmap.go:11-21)
+    is pinned read-only, decoded through the pipeline and unpinned."""
+    import mmap
+    monkeypatch.setenv("LSMGPU_HOST_CHUNK", "1048576")
+    c2 = _cols(2, 60000, seed=71)
+    body, _, _ = oracle.build_cols(c2.keys, c2.key_end, c2.vs, c2.vs_end, 0, 4096)
+    sst = body + b"{}" + (2).to_bytes(4, "big")
+    path = tmp_path / "000001.sst"
+    path.write_bytes(sst)
+    off, ln, _, _ = oracle.parse_index(sst)
+    ref = oracle.decode(sst, off, ln)
+    with open(path, "rb") as f:
+        mm = mmap.mmap(f.fileno(), 0, prot=mmap.PROT_READ)
+        arr = np.frombuffer(mm, np.uint8)
+        codec.host_register(arr)
+        try:
+            g = codec.decode_host(arr, off, ln)
+        finally:
+            codec.host_unregister(arr)
+        _check(g, ref, 3, "read-only mmap")
+        del arr
+        mm.close()
+
+
+def test_host_register_foreign_pinned(codec, mixed, monkeypatch):
+    """Memory page-locked outside the library (torch's pinned allocator, hipHostMalloc) is not
+    registered again: LSMGPU_ERR_HOST_PINNED, and it decodes as it is."""
+    import torch
+    monkeypatch.setenv("LSMGPU_HOST_CHUNK", "1048576")
+    data, off, ln, ref = mixed
+    t = torch.empty(len(data), dtype=torch.uint8, pin_memory=True)
+    arr = t.numpy()
+    arr[:] = np.frombuffer(data, np.uint8)
+    rc = _lib.lib().lsmgpu_host_register(codec._ctx, _ptr(arr), arr.nbytes)
+    assert rc == _lib.ERR_HOST_PINNED
+    _check(codec.decode_host(arr, off, ln), ref, 3, "foreign pinned")
+    assert _lib.lib().lsmgpu_host_unregister(codec._ctx, _ptr(arr)) == _lib.ERR_ARG
 
 
 def _decode_raw(codec, data, off, ln, mode, key_cap, val_cap, ent_cap):
@@ -144,4 +228,3 @@ def test_host_pipeline_fallbacks(codec, oracle, monkeypatch):
     ref = oracle.decode(full, o3, l3)
     assert ref.key_data.size > len(full)
     _assert_same(codec.decode_host(full, o3, l3), ref, "expanding keys")
-    _ = ctypes
