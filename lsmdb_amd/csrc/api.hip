@@ -56,10 +56,37 @@ PinRegistry& pins() {
   return r;
 }
 
+// A host copy HIP refuses (hipErrorInvalidValue: its pinned-memory bookkeeping disagrees with the
+// pages -- seen on buffers re-registered at re-used heap addresses) is done through this thread's
+// page-locked bounce buffer instead: the runtime never sees the caller's address, and the call
+// stays correct whatever the runtime believes about it.  Synchronous on the stream.
+constexpr uint64_t kBounce = 8ull << 20;
+hipError_t bounce_copy(void* dst, const void* src, uint64_t n, hipMemcpyKind kind, hipStream_t s) {
+  thread_local uint8_t* buf = nullptr;
+  if (!buf && hipHostMalloc(reinterpret_cast<void**>(&buf), kBounce, hipHostMallocPortable) != hipSuccess) {
+    buf = nullptr;
+    return hipErrorOutOfMemory;
+  }
+  hipError_t e = hipStreamSynchronize(s);  // the bounce buffer is free, earlier work is done
+  for (uint64_t o = 0; o < n && e == hipSuccess; o += kBounce) {
+    const uint64_t m = std::min(kBounce, n - o);
+    if (kind == hipMemcpyHostToDevice) {
+      std::memcpy(buf, static_cast<const uint8_t*>(src) + o, m);
+      e = hipMemcpyAsync(static_cast<uint8_t*>(dst) + o, buf, m, kind, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+    } else {
+      e = hipMemcpyAsync(buf, static_cast<const uint8_t*>(src) + o, m, kind, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e == hipSuccess) std::memcpy(static_cast<uint8_t*>(dst) + o, buf, m);
+    }
+  }
+  return e;
+}
+
 // hipMemcpyAsync between HBM and a host range, cut where pinned segments begin and end: HIP serves
 // a copy from the registration its first byte lies in and rejects one that runs past that
 // registration's end (a buffer whose edge pages another caller pinned, or a neighbour's).  Every
-// host copy of the library goes through here.
+// host copy of the library goes through here; a piece HIP refuses goes through bounce_copy.
 hipError_t hcopy(void* dst, const void* src, uint64_t n, hipMemcpyKind kind, hipStream_t s) {
   if (!n) return hipSuccess;
   const bool h2d = kind == hipMemcpyHostToDevice;
@@ -70,12 +97,41 @@ hipError_t hcopy(void* dst, const void* src, uint64_t n, hipMemcpyKind kind, hip
   std::shared_lock<std::shared_mutex> g(pins().mu());
   pins().pieces(h, n, &pc);
   for (const auto& r : pc) {
-    const uint64_t o = r.first - h;
-    hipError_t e = hipMemcpyAsync(static_cast<uint8_t*>(dst) + o, static_cast<const uint8_t*>(src) + o,
-                                  r.second - r.first, kind, s);
+    const uint64_t o = r.first - h, m = r.second - r.first;
+    void* d = static_cast<uint8_t*>(dst) + o;
+    const void* q = static_cast<const uint8_t*>(src) + o;
+    hipError_t e = hipMemcpyAsync(d, q, m, kind, s);
+    if (e == hipErrorInvalidValue) {
+      static const bool dbg = getenv("LSMGPU_DEBUG_ERR") != nullptr;
+      if (dbg)
+        fprintf(stderr, "lsmgpu: hcopy %s host piece [%#lx, %#lx) of [%#lx, %#lx) refused (%s): bounce\n",
+                h2d ? "H2D" : "D2H", (unsigned long)r.first, (unsigned long)r.second,
+                (unsigned long)h, (unsigned long)(h + n), hipGetErrorString(e));
+      (void)hipGetLastError();
+      e = bounce_copy(d, q, m, kind, s);
+    }
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+// Memory page-locked outside this library (hipHostMalloc, a caller's hipHostRegister): the
+// runtime reports it as host memory.  Caller holds the registry lock; ptrs inside our own
+// segments are not foreign.
+bool pinned_elsewhere(const void* p) {
+  hipPointerAttribute_t a{};
+  const hipError_t e = hipPointerGetAttributes(&a, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+// LSMGPU_DEBUG_PIN=1: every pin / unpin of a segment on stderr (diagnostics)
+bool debug_pin() {
+  static const bool on = getenv("LSMGPU_DEBUG_PIN") != nullptr;
+  return on;
 }
 
 // Synchronizes the given streams when the scope ends, on every return path: a call that returns
@@ -403,6 +459,16 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     p.wkeep = vk_env && atoi(vk_env) == 0 ? 0u : 1u;
     const char* wt_env = getenv("LSMGPU_WSC_TILE");  // A/B: lane-walk workgroup of 192 / 256
     p.wtile = wt_env && atoi(wt_env) == 192 ? 192u : 256u;
+    // lane walks: 576-block tiles (9 waves, 2 workgroups per CU) when 256-block ones (4 per CU,
+    // LDS-bound) would not all be resident at once and 576-block ones would -- a second wave of
+    // tiles walks its ~31 dependent hops at low load (C2 2^30 B: 1,041 tiles of 256 for 1,024
+    // slots; same box: walk 0.2296 -> 0.210 ms, view 0.258 -> 0.233 ms, decode 1,365 -> 1,400
+    // GiB/s, profiles/r05c, r05d, r05e).  With every 256-block tile resident the wide tile is
+    // slightly slower (walk 0.2005 vs 0.2036 ms).  LSMGPU_WSC_WIDE=0 / 1 forces it off / on.
+    const char* ww_env = getenv("LSMGPU_WSC_WIDE");
+    const uint64_t cus = (uint64_t)c->num_cus;
+    p.wwide = ww_env ? (atoi(ww_env) != 0 ? 576u : 0u)
+                     : ((nblk + 255) / 256 > 4 * cus && (nblk + 575) / 576 <= 2 * cus ? 576u : 0u);
 
     const char* wk_env = getenv("LSMGPU_WSC_WALK");
     // Default: 8 lanes per block guessing same-shape runs (kWalkGroup) when the batch has at
@@ -467,6 +533,11 @@ int lsmgpu_host_register(lsmgpu_ctx* c, void* p, uint64_t bytes) {
   std::unique_lock<std::shared_mutex> g(R.mu());
   // pin only the pages no segment covers yet, each run as a segment of its own
   const std::vector<PinRegistry::Range> gaps = R.gaps((uintptr_t)p, bytes);
+  // a gap the runtime already knows as page-locked memory was pinned outside the library
+  for (const auto& gp : gaps)
+    if (pinned_elsewhere(reinterpret_cast<void*>(std::max<uintptr_t>(gp.first, (uintptr_t)p))) ||
+        pinned_elsewhere(reinterpret_cast<void*>(std::min<uintptr_t>(gp.second, (uintptr_t)p + bytes) - 1)))
+      return LSMGPU_ERR_HOST_PINNED;
   std::vector<PinRegistry::Range> made;
   int rc = LSMGPU_OK;
   for (const auto& gp : gaps) {
@@ -485,6 +556,9 @@ int lsmgpu_host_register(lsmgpu_ctx* c, void* p, uint64_t bytes) {
       rc = e == hipErrorHostMemoryAlreadyRegistered ? LSMGPU_ERR_HOST_PINNED : LSMGPU_ERR_HIP;
       break;
     }
+    if (debug_pin())
+      fprintf(stderr, "lsmgpu: pin [%#lx, %#lx) for [%p, +%llu)\n", (unsigned long)gp.first,
+              (unsigned long)gp.second, p, (unsigned long long)bytes);
     made.push_back(gp);
   }
   if (rc != LSMGPU_OK) {
@@ -515,6 +589,9 @@ int lsmgpu_host_unregister(lsmgpu_ctx* c, void* p) {
   }
   int rc = LSMGPU_OK;
   for (const auto& r : unpin) {
+    if (debug_pin())
+      fprintf(stderr, "lsmgpu: unpin [%#lx, %#lx) (recut %d)\n", (unsigned long)r.first,
+              (unsigned long)r.second, (int)recut);
     hipError_t e = hipHostUnregister(reinterpret_cast<void*>(r.first));
     if (e != hipSuccess) {
       report_hip_error("hipHostUnregister", e, __LINE__);

@@ -157,17 +157,26 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
 // after the look-back each wave writes its 64 blocks' view records from LDS (records past
 // kViewRec, rare, go to / come from p.wmeta)
 // SLOT: the staged walk's LDS bytes per block
+// WIDE (TB = 576, lane walks): 9-wave workgroups of 576 blocks, 2 per CU = 1,152 blocks per CU in
+// flight, against 4 x 256 = 1,024 for TB = 256 (LDS-bound: 33 words per lane).  (384-block tiles,
+// 51 KB, are not 3 per CU: walk 0.267 ms, profiles/r05e -- as if a workgroup's LDS had to lie in
+// one 80 KB half of the CU's 160 KB, which also fits round 4's census of 3 x 54 KB.)  C2 at 2^30 B has
+// 266,403 blocks: 1,041 tiles of 256 for 1,024 resident slots, and the 17-tile second wave cost
+// the walk 0.030 ms and the view decode 0.045 ms (same-box A/B, profiles/r05c); 463 tiles of 576
+// are all resident.  WIDE keeps no per-lane tables besides the rows (no s_first / s_off).
 template <int MODE, uint32_t TB, uint32_t CH = 32, uint32_t SLOT = kStageSlot>  // TB = blocks per tile
-__global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
-  static_assert(TB <= 256, "one thread per block of the tile");
+__global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) wsc_walk_kernel(DecodeParams p) {
+  constexpr bool WIDE = MODE != kWalkGroup && TB > 256;
+  static_assert(TB <= 256 || (WIDE && TB <= 1024 && CH == 32), "one thread per block of the tile");
   static_assert(CH == 16 || CH == 32, "16 or 32 records per chunk");
   constexpr bool KEEP = MODE == kWalkLaneView;
-  // lane walks: one thread per block, TB = 192 or 256 threads; the group walk: 256 threads
+  // lane walks: one thread per block, TB = 192, 256 or 576 threads; the group walk: 256 threads
   constexpr uint32_t kThreads = MODE == kWalkGroup ? 256 : TB;
   constexpr uint32_t kWaves = kThreads / 64;
   static_assert(kThreads % 64 == 0, "whole waves");
-  // LDS row per lane: CH records (+ 1 pad, bank spread), or kViewRec kept records (+ 1)
-  constexpr uint32_t kStage = KEEP ? kViewRec + 1 : CH + 1;
+  // LDS row per lane: CH records (+ 1 pad, bank spread), or kViewRec kept records (+ 1; WIDE:
+  // none, the 33-word stride is odd already)
+  constexpr uint32_t kStage = KEEP ? (WIDE ? kViewRec : kViewRec + 1) : CH + 1;
   constexpr uint32_t kStageBytes = kThreads * kStage * sizeof(uint32_t);
   // group walk: a 32-record ring per block (the walk's LDS also serves the view epilogue's
   // owner map)
@@ -189,13 +198,14 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   __shared__ uint32_t s_tile;
   __shared__ uint32_t s_wave[kWaves][3];
   __shared__ uint32_t s_ex[3];
-  __shared__ uint32_t s_first[KEEP ? 1 : kThreads + 1];  // p.wfuse: tile-relative first entry
-  __shared__ uint32_t s_off[MODE == kWalkGroup ? TB : kThreads];  // each block's input offset
+  __shared__ uint32_t s_first[KEEP || WIDE ? 1 : kThreads + 1];  // p.wfuse: tile-relative first entry
+  // each block's input offset (group walks; the lane walk's non-kept view epilogue)
+  __shared__ uint32_t s_off[MODE == kWalkGroup ? TB : (KEEP || WIDE ? 1 : kThreads)];
   constexpr uint32_t kRes = MODE == kWalkGroup ? TB : 1;
   __shared__ uint32_t s_res[4][kRes];  // group / wave walk: n, K, V, status per block
   __shared__ uint32_t s_stg[kRes];  // group walk: the block is in its LDS slot (kStaged)
   __shared__ uint32_t s_cb[3][kWave64 ? TB : 1];  // p.wscopy: each block's output bases
-  __shared__ uint32_t s_mark[KEEP ? kWaves : 1][128];  // kWalkLaneView, p.wview: owner marks
+  __shared__ uint8_t s_mark[KEEP ? kWaves : 1][128];  // kWalkLaneView, p.wview: owner marks (lane + 1)
   // the staged walk copying its own blocks (p.wscopy): no records for a copy launch
   const bool scopy = kWave64 && p.wscopy && !p.wfuse;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
@@ -215,6 +225,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   // thread t owns block tile * TB + t (threads past TB own none: zero entries)
   const uint32_t b = tid < TB ? tile * TB + tid : 0xffffffffu;
   uint32_t n = 0, K = 0, V = 0, st = LSMGPU_BLK_OK;
+  uint32_t lane_off = 0;  // lane walks: this thread's block offset
   if constexpr (MODE == kWalkGroup) {
     // L lanes per block: each round the group reads the headers at pos + k * stride (stride =
     // the last accepted entry's size) and accepts the leading run whose guesses were right --
@@ -425,7 +436,8 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     if (valid) {
       off = p.blk_off[b];
       len = p.blk_len[b];
-      s_off[tid] = off;
+      if constexpr (!KEEP && !WIDE) s_off[tid] = off;  // the non-kept view epilogue's table
+      lane_off = off;
     }
     bool done = !valid || (p.ablate & 4);  // (timing-only ablation 4: no walk)
     if (valid && (uint64_t)off + len > p.data_len) {
@@ -541,7 +553,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
   }
   __syncthreads();
   uint32_t en_b = 0;  // this thread's block's first entry (kWalkLaneView's view loop)
-  const uint32_t off_b = (MODE != kWalkGroup && b < p.nblk) ? s_off[tid] : 0u;
+  const uint32_t off_b = MODE != kWalkGroup ? lane_off : 0u;
   if (b < p.nblk) {
     uint32_t on = s_ex[0], ok = s_ex[1], ov = s_ex[2];
     for (uint32_t w = 0; w < wave; w++) {
@@ -636,7 +648,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
       // owners by one scatter and a max-scan, two passes (128 entries) per trip: every block
       // with entries marks (lane + 1) at its first entry's slot, a DPP max-scan carries the
       // marks forward (the previous pass's last owner carried in)
-      uint32_t* const mk = s_mark[KEEP ? wave : 0];
+      uint8_t* const mk = s_mark[KEEP ? wave : 0];
       mk[lane] = 0;
       mk[64 + lane] = 0;
       wave_lds_fence();
@@ -671,6 +683,7 @@ __global__ void __launch_bounds__(256) wsc_walk_kernel(DecodeParams p) {
     }
     return;
   }
+  if constexpr (WIDE) return;  // (never launched with the non-kept view epilogue below)
   // View-only decode (p.wfuse): the workgroup writes its tile's dense view records itself, so
   // no copy launch follows.  Output entry e of the tile belongs to the last block whose first
   // entry is <= e (binary search over s_first); its record comes from the walk metadata this
@@ -968,6 +981,10 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 16>), dim3((nblk + 15) / 16), dim3(256), 0, s, p);
   else if (p.wwalk == kWalkGroup)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 32>), dim3((nblk + 31) / 32), dim3(256), 0, s, p);
+  else if (p.wfuse && p.wkeep && p.wwide == 576)
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkLaneView, 576>), dim3((nblk + 575) / 576), dim3(576), 0, s, p);
+  else if (!p.wfuse && p.wwide == 576 && p.wchunk == 32)
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 576>), dim3((nblk + 575) / 576), dim3(576), 0, s, p);
   else if (p.wfuse && p.wkeep && p.wtile == 192)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLaneView, 192>), dim3((nblk + 191) / 192), dim3(192), 0, s, p);
   else if (p.wfuse && p.wkeep)

@@ -504,7 +504,7 @@ def test_wsc_lanes_per_entry(codec, oracle, monkeypatch, lanes):
     _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln), f"J={lanes}")
 
 
-@pytest.mark.parametrize("walk", ["lane", "lane16", "lane192", "lane_flush", "lane_viewsearch", "group", "group2",
+@pytest.mark.parametrize("walk", ["lane", "lane16", "lane192", "lane576", "lane_flush", "lane_viewsearch", "group", "group2",
                                   "group4", "group16", "group32", "group64", "group64_copy", "group64s",
                                   "group64g", "group64g_copy", "group_sub", "group16_sub",
                                   "group_dpp"])
@@ -524,6 +524,9 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     elif walk == "lane192":  # lane-walk workgroups of 192 blocks
         monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
         monkeypatch.setenv("LSMGPU_WSC_TILE", "192")
+    elif walk == "lane576":  # wide lane-walk tiles (576 blocks, 9 waves: the 2^30-B default)
+        monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
+        monkeypatch.setenv("LSMGPU_WSC_WIDE", "1")
     elif walk == "lane_viewsearch":  # view-only: owners by lane-shuffle binary search
         monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
         monkeypatch.setenv("LSMGPU_WSC_VIEWSCAN", "0")
@@ -633,7 +636,7 @@ def _block_entries(block):
     return out
 
 
-@pytest.mark.parametrize("walk", ["lane", "lane16", "lane192", "group", "group32", "group64",
+@pytest.mark.parametrize("walk", ["lane", "lane16", "lane192", "lane576", "group", "group32", "group64",
                                   "group64g", "group_sub"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
@@ -646,7 +649,9 @@ def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
     oracle's iterator does."""
     from lsmdb_amd.codec import MODE_MATERIALIZE, MODE_VIEW
     monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
-    monkeypatch.setenv("LSMGPU_WSC_WALK", "lane" if walk in ("lane16", "lane192") else walk.replace("_sub", ""))
+    monkeypatch.setenv("LSMGPU_WSC_WALK", "lane" if walk in ("lane16", "lane192", "lane576")
+                       else walk.replace("_sub", ""))
+    monkeypatch.setenv("LSMGPU_WSC_WIDE", "1" if walk == "lane576" else "0")
     monkeypatch.setenv("LSMGPU_WSC_SUB", "1" if walk.endswith("_sub") else "0")
     if walk == "group64g":
         monkeypatch.setenv("LSMGPU_WSC_WALK", "group64")

@@ -2,7 +2,7 @@
 
 * decodeTable: parse_index size query -> allocate -> parse_index; newDecodedBatch with upper
   bounds -> decode_blocks (-> the reported needs and a second decode_blocks only on
-  LSMGPU_ERR_CAPACITY); optionally pinned first (pinMmap).  Checked against the oracle's decode
+  LSMGPU_ERR_CAPACITY); optionally pinned for the call (decodeTablePinned).  Checked against the oracle's decode
   of the same blocks (table/iterator.go:93-135).
 * finishBlocks: encode_blocks size query (out == NULL) -> allocate out_len -> encode_blocks.
   Checked byte for byte against the oracle Builder (table/builder.go:84-198).
@@ -29,7 +29,7 @@ def shim_decode_table(ctx, sst: bytes, pin: bool = False):
     """decodeTable step by step: tail parse, upper-bound buffers (entries <=
     data/10, key and value bytes <= data), one decode; on LSMGPU_ERR_CAPACITY (prefix-compressed
     keys that expand) the reported needs are allocated and the decode repeated.  pin: the
-    table's bytes page-locked first (pinMmap).  Returns the host SoA, the final call's needs,
+    table's bytes page-locked around the decode (decodeTablePinned: register, decode, unregister).  Returns the host SoA, the final call's needs,
     the block list and the number of decode calls made."""
     L = _lib.lib()
     base = np.frombuffer(sst + b"\0", np.uint8).copy()
@@ -42,8 +42,8 @@ def shim_decode_table(ctx, sst: bytes, pin: bool = False):
                                 byref(bo), byref(bl)) == _lib.OK
     n = nblk.value
     data_end = int(off[n - 1]) + int(ln[n - 1]) if n else 0
-    if pin:
-        assert L.lsmgpu_host_register(ctx, _ptr(base), base.size) == _lib.OK
+    pinned = pin and L.lsmgpu_host_register(ctx, _ptr(base), base.size) == _lib.OK
+    assert pinned == pin  # plain numpy memory: the registration succeeds
 
     def batch(entries, kbytes, vbytes):  # newDecodedBatch
         arrs = dict(kd=np.zeros(max(kbytes, 1), np.uint8), vd=np.zeros(max(vbytes, 1), np.uint8),
@@ -65,7 +65,7 @@ def shim_decode_table(ctx, sst: bytes, pin: bool = False):
         d, arrs = batch(d.n_entries, d.key_bytes, d.val_bytes)
         rc = L.lsmgpu_decode_blocks(ctx, _ptr(base), data_end, 0, _ptr(off), _ptr(ln), n, MAT_VIEW,
                                     byref(d))
-    if pin:
+    if pinned:
         assert L.lsmgpu_host_unregister(ctx, _ptr(base)) == _lib.OK
     assert rc == _lib.OK
     m = d.n_entries
