@@ -134,7 +134,9 @@ int lsmgpu_decode_blocks(lsmgpu_ctx* ctx, const uint8_t* data, uint64_t data_len
  * mappings are pinned read-only -- or LoadToRAM's heap buffer, table.go:117-123,329-338) and
  * large output arrays with lsmgpu_host_register, unpin with lsmgpu_host_unregister(p) (the same
  * pointer) before the memory is freed or unmapped.
- * Pinning is page-granular.  The library keeps one process-wide registry of page-aligned
+ * Pinning is page-granular: the whole pages inside the range are pinned, its partial first and
+ * last pages are not (they may hold other allocations' bytes; copies of those < 2 pages are
+ * staged by the runtime).  The library keeps one process-wide registry of page-aligned
  * segments, each pinned once: a range pins only its pages no earlier registration covers and
  * references every segment it overlaps, so ranges may share pages, nest, repeat and come back
  * at re-used addresses; a segment is unpinned when its last range is unregistered.  Every host

@@ -465,6 +465,10 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     // slots; same box: walk 0.2296 -> 0.210 ms, view 0.258 -> 0.233 ms, decode 1,365 -> 1,400
     // GiB/s, profiles/r05c, r05d, r05e).  With every 256-block tile resident the wide tile is
     // slightly slower (walk 0.2005 vs 0.2036 ms).  LSMGPU_WSC_WIDE=0 / 1 forces it off / on.
+    // copy: blocks of <= 63 entries write their key and value streams as aligned 16-B chunks
+    // (copy_stream_aligned); LSMGPU_WSC_ALIGN=0 keeps the unaligned 16-B pieces
+    const char* al_env = getenv("LSMGPU_WSC_ALIGN");
+    p.walign = al_env && atoi(al_env) == 0 ? 0u : 1u;
     const char* ww_env = getenv("LSMGPU_WSC_WIDE");
     const uint64_t cus = (uint64_t)c->num_cus;
     p.wwide = ww_env ? (atoi(ww_env) != 0 ? 576u : 0u)
@@ -578,15 +582,19 @@ int lsmgpu_host_unregister(lsmgpu_ctx* c, void* p) {
   std::vector<PinRegistry::Range> unpin, repin;
   bool recut = false;
   if (!R.remove((uintptr_t)p, &unpin, &repin, &recut)) return LSMGPU_ERR_ARG;  // not registered here
-  if (recut) {
-    // a segment other ranges still use in part is unpinned and its covered runs pinned again:
-    // drain every device first (no copy from those pages in flight; new copies wait on the lock)
+  if (!unpin.empty()) {
+    // drain every device before unpinning: no copy from those pages may be in flight (a re-cut
+    // unpins pages other ranges still use; new copies wait on the lock), and the runtime releases
+    // a registration whose copies have all retired at once, not later -- a deferred release could
+    // otherwise unpin pages a later registration of the same addresses has pinned again
     int ndev = 0;
     (void)hipGetDeviceCount(&ndev);
     for (int d = 0; d < ndev; d++)
       if (hipSetDevice(d) == hipSuccess) (void)hipDeviceSynchronize();
     (void)hipSetDevice(c->device);
+    (void)hipGetLastError();
   }
+  (void)recut;
   int rc = LSMGPU_OK;
   for (const auto& r : unpin) {
     if (debug_pin())

@@ -838,6 +838,75 @@ __device__ __forceinline__ void copy_entries(const DecodeParams& p, const uint32
   }
 }
 
+// One output stream (keys or values) of a block with n <= 63 entries and no prefix-compressed
+// entry, written as ALIGNED 16-B chunks (round 5).  The copy's unaligned, overlapping 16-B pieces
+// reach L2 as ~54-B write requests (19.9 M per C2 1 GiB copy vs 8.4 M 128-B ones for a streaming
+// copy of the same bytes, profiles/r05g); with aligned chunks every store instruction writes whole
+// lines (per-block probe, scripts/align_probe.hip: 0.41-0.44 vs 0.49-0.56 ms).  Stream position u
+// (relative to the block's first byte in the stream, at address B) of entry e comes from block
+// byte src_e + u - so_e; lane e (< n) holds so_e (the entry's stream offset) and src_e, lanes >= n
+// hold so = S (the block's stream length).  Chunk i covers [u0 + 16 i, +16) with B + u0 16-B
+// aligned; its lane finds the last entry e with so_e <= u by a lane-shuffle binary search, loads 16
+// bytes from e's source and merges the bytes of the entries after e (one more load each, in place
+// under byte masks: the load starts k bytes before the next entry's first byte, k = bytes taken so
+// far).  Every load stays inside the block: from e at offset >= 0, from later entries at most 15
+// bytes before their first byte (their header and key precede it), never past a full chunk's
+// last byte.  The <= 15 bytes before u0 and after the last whole chunk share their 16-B chunks with
+// the neighbouring blocks' streams: one lane per byte.
+__device__ __forceinline__ uint32_t bytes_below(uint32_t k, uint32_t d) {  // mask of dword d's bytes < k
+  const int32_t t = (int32_t)k - 4 * (int32_t)d;
+  return t >= 4 ? 0xffffffffu : t <= 0 ? 0u : (1u << (8 * t)) - 1u;
+}
+__device__ __forceinline__ void copy_stream_aligned(uint8_t* B, uint32_t S, uint32_t so, uint32_t src,
+                                                    uint32_t n, const uint8_t* blk, uint32_t lane) {
+  if (S == 0) return;
+  const uint32_t u0 = min((uint32_t)((16u - ((uintptr_t)B & 15u)) & 15u), S);
+  const uint32_t nfull = (S - u0) >> 4;
+  auto owner = [&](uint32_t u) -> uint32_t {  // the last entry e < n with so_e <= u (so_0 = 0)
+    uint32_t L = 0;
+#pragma unroll
+    for (uint32_t st = 32; st >= 1; st >>= 1) {
+      const uint32_t cand = L + st;
+      const uint32_t sc = (uint32_t)__shfl((int)so, (int)min(cand, 63u));
+      if (cand < n && sc <= u) L = cand;
+    }
+    return L;
+  };
+  for (uint32_t i0 = 0; i0 < nfull; i0 += kWave) {
+    const bool on = i0 + lane < nfull;
+    const uint32_t u = u0 + 16u * min(i0 + lane, nfull - 1);
+    const uint32_t e = owner(u);
+    const uint32_t so_e = (uint32_t)__shfl((int)so, (int)e), src_e = (uint32_t)__shfl((int)src, (int)e);
+    uint32_t k = (uint32_t)__shfl((int)so, (int)e + 1) - u;  // bytes of the chunk from entry e
+    uint4 w;
+    __builtin_memcpy(&w, blk + src_e + (u - so_e), 16);
+    uint32_t f = e + 1;
+    while (__ballot(on && k < 16u)) {  // entries after e (uniform: every lane shuffles)
+      const uint32_t fc = min(f, 62u);
+      const uint32_t src_f = (uint32_t)__shfl((int)src, (int)fc);
+      const uint32_t so_f1 = (uint32_t)__shfl((int)so, (int)fc + 1);
+      if (on && k < 16u) {
+        uint4 w2;
+        __builtin_memcpy(&w2, blk + src_f - k, 16);
+        w.x = (w.x & bytes_below(k, 0)) | (w2.x & ~bytes_below(k, 0));
+        w.y = (w.y & bytes_below(k, 1)) | (w2.y & ~bytes_below(k, 1));
+        w.z = (w.z & bytes_below(k, 2)) | (w2.z & ~bytes_below(k, 2));
+        w.w = (w.w & bytes_below(k, 3)) | (w2.w & ~bytes_below(k, 3));
+        k = so_f1 - u;
+      }
+      f++;
+    }
+    if (on) *reinterpret_cast<uint4*>(B + u) = w;
+  }
+  // the head [0, u0) and the tail [u0 + 16 nfull, S): one lane per byte
+  const uint32_t ut = u0 + 16u * nfull;
+  const bool hb = lane < 16 ? lane < u0 : (lane < 32 && ut + (lane - 16) < S);
+  const uint32_t q = min(lane < 16 ? lane : ut + (lane - 16), S - 1);
+  const uint32_t e = owner(q);
+  const uint32_t so_e = (uint32_t)__shfl((int)so, (int)e), src_e = (uint32_t)__shfl((int)src, (int)e);
+  if (hb) B[q] = blk[src_e + q - so_e];
+}
+
 // A block with prefix-compressed entries (plen > 0: never written by Builder; the
 // format the iterator accepts): entries 64 at a time, lane = entry, plen read from the header,
 // key offsets by a wave scan of plen + stored key bytes; keys bytewise as baseKey[:plen] ++ diff
@@ -931,7 +1000,18 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
   // (round 4: each lane's first piece of every entry of a pass loaded before any store left
   // the copy unchanged, 0.6038 vs 0.6042 ms, profiles/r04c; compiled into this kernel it also
   // raised the VGPRs from 44 to 90, 8 -> 5 waves per SIMD: removed)
-  if (p.wj == 16 || (p.wj == 0 && avg > 128)) {
+  if (p.walign && mat && split == 1 && n < kWave) {
+    // aligned output chunks (copy_stream_aligned): records 0 .. n sit one per lane in `pre`
+    entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
+    const uint32_t m1 = (uint32_t)__shfl((int)pre, (int)min(lane + 1, kWave - 1));
+    const uint32_t hp = pre & 0xffffu, vo = pre >> 16, hp1 = m1 & 0xffffu, vo1 = m1 >> 16;
+    const uint32_t vl = vo1 - vo, kl = hp1 - hp - 10 - vl;
+    const bool ent = lane < n;
+    if (kbase)
+      copy_stream_aligned(kbase, K, ent ? hp - 10 * lane - vo : K, hp + 10, n, blk, lane);
+    if (vbase)
+      copy_stream_aligned(vbase, V, ent ? vo : V, hp + 10 + kl, n, blk, lane);
+  } else if (p.wj == 16 || (p.wj == 0 && avg > 128)) {
     copy_entries<16, 2, true>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
   } else {
     entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);

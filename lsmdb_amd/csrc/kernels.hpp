@@ -53,6 +53,7 @@ struct DecodeParams {
   uint32_t wchunk;          // lane walk: records per flushed chunk (16 or 32)
   uint32_t wkeep;           // view-only lane walk: records kept in LDS (kWalkLaneView)
   uint32_t wtile;           // lane walks: blocks (= threads) per workgroup, 192 or 256
+  uint32_t walign;          // copy: aligned 16-B output chunks for blocks of <= 63 entries
   uint32_t wwide;           // lane walks: 0 (256-block tiles, 4 per CU) or 576 (2 per CU)
   uint32_t wscopy;          // 64-lane staged group walk: each wave copies its block from LDS
   uint32_t wslot;           // 64-lane staged group walk: 0 = kStageSlot, 1 = kStageSlotSmall

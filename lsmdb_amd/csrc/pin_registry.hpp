@@ -7,9 +7,10 @@
 //  * pinning is page-granular, and a page must not be registered twice;
 //  * a host copy is served from the registration its FIRST byte lies in, and one that runs past
 //    that registration's end is rejected.
-// So the library pins page-aligned, pairwise-disjoint SEGMENTS, each its own hipHostRegister.  A
-// caller's range uses (references) every segment its pages overlap, and registering a range pins
-// only the pages no segment covers yet.  Invariant: every pinned page lies in the pages of some
+// So the library pins page-aligned, pairwise-disjoint SEGMENTS, each its own hipHostRegister, made
+// of whole pages inside the callers' ranges (a range's partial first and last pages are never
+// pinned: they may belong to other allocations).  A caller's range uses (references) every segment
+// its pages overlap, and registering a range pins only the pages no segment covers yet.  Invariant: every pinned page lies in the pages of some
 // live range.  When a range goes, a segment no live range overlaps is unpinned, and a segment
 // other ranges still overlap only in part is RE-CUT (unpinned, its still-covered page runs pinned
 // again): leaving it whole would keep pages of a freed buffer pinned, and a buffer mapped there
@@ -42,11 +43,16 @@ class PinRegistry {
   size_t segments() const { return segs_.size(); }
   size_t users() const { return uses_.size(); }
 
-  // [p, p + bytes) rounded out to whole pages.
+  // The whole pages inside [p, p + bytes) (possibly none).  Only those are pinned: the partial
+  // first and last pages may hold other allocations' bytes (heap neighbours, the decode's own
+  // output arrays allocated next to the input), and no copy into or out of such bytes may be
+  // served through this registration's mapping -- round 5's GPU suite faulted (illegal memory
+  // access in the pipeline's first device-to-host copy) with the ranges rounded OUT to pages.
+  // The edge pieces (< 1 page each) are copied as pageable memory.
   Range page_range(uintptr_t p, uint64_t bytes) const {
-    const uintptr_t a = p / page_ * page_;
-    const uintptr_t e = (p + bytes + page_ - 1) / page_ * page_;
-    return {a, e};
+    const uintptr_t a = (p + page_ - 1) / page_ * page_;
+    const uintptr_t e = (p + bytes) / page_ * page_;
+    return a < e ? Range{a, e} : Range{a, a};
   }
 
   // The page-aligned runs of [p, p + bytes)'s pages that no segment covers: what a register must
@@ -54,6 +60,7 @@ class PinRegistry {
   std::vector<Range> gaps(uintptr_t p, uint64_t bytes) const {
     const Range pr = page_range(p, bytes);
     std::vector<Range> out;
+    if (pr.first >= pr.second) return out;
     uintptr_t cur = pr.first;
     auto it = first_overlapping(cur);
     while (cur < pr.second) {
@@ -73,8 +80,9 @@ class PinRegistry {
   void add(uintptr_t p, uint64_t bytes, const std::vector<Range>& made) {
     for (const Range& m : made) segs_[m.first] = Seg{m.second, 0};
     const Range pr = page_range(p, bytes);
-    for (auto it = first_overlapping(pr.first); it != segs_.end() && it->first < pr.second; ++it)
-      it->second.refs++;
+    if (pr.first < pr.second)  // (a range without a whole page uses no segment)
+      for (auto it = first_overlapping(pr.first); it != segs_.end() && it->first < pr.second; ++it)
+        it->second.refs++;
     uses_.emplace(p, pr);
   }
 
@@ -92,7 +100,8 @@ class PinRegistry {
     const Range pr = u->second;
     uses_.erase(u);
     std::vector<Range> recut;
-    for (auto it = first_overlapping(pr.first); it != segs_.end() && it->first < pr.second;) {
+    for (auto it = pr.first < pr.second ? first_overlapping(pr.first) : segs_.end();
+         it != segs_.end() && it->first < pr.second;) {
       const Range sg{it->first, it->second.e};
       if (--it->second.refs == 0) {
         unpin->push_back(sg);

@@ -6,6 +6,8 @@
 //   merged : one lane per ALIGNED 16-B output chunk of the value stream; its bytes come from one
 //            or two entries: two unaligned loads, the second from (next value - x) so its bytes
 //            already sit at their window positions, merged with v_bfi under byte masks
+//   merged32: the same with 32-bit index math (entry = chunk * 16 / 103 by a float reciprocal and
+//            one correction step; round 3's form divided 64-bit integers per lane)
 // Build: hipcc --offload-arch=gfx950 -O3 -o scripts/merge_store_probe scripts/merge_store_probe.hip
 #include <hip/hip_runtime.h>
 
@@ -72,6 +74,37 @@ __global__ void __launch_bounds__(256) merged(const uint8_t* __restrict__ s, uin
   }
 }
 
+__global__ void __launch_bounds__(256) merged32(const uint8_t* __restrict__ s, uint8_t* __restrict__ kd,
+                                                uint8_t* __restrict__ vd, uint32_t n) {
+  const uint32_t gl = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t stride = gridDim.x * 256;
+  const uint32_t nk = n, nv = (uint32_t)((uint64_t)n * kVal / 16);
+  for (uint32_t t = gl; t < nk + nv; t += stride) {
+    if (t < nk) {
+      const uint4 v = ld16(s + (uint64_t)t * kEnt + 10);
+      *reinterpret_cast<uint4*>(kd + (uint64_t)t * kKey) = v;
+      continue;
+    }
+    const uint32_t c = t - nk, w = 16 * c;
+    uint32_t e = (uint32_t)((float)w * (1.0f / kVal));
+    if (e * kVal > w) e--;
+    if ((e + 1) * kVal <= w) e++;
+    const uint32_t o = w - e * kVal;
+    const int32_t x = (int32_t)min(16u, kVal - o);
+    const uint8_t* pe = s + (uint64_t)e * kEnt + 10 + kKey;
+    const uint4 a = ld16(pe + o);
+    uint4 out = a;
+    if (x < 16 && e + 1 < n) {
+      const uint4 b = ld16(pe + kEnt - x);
+      out.x = (a.x & bmask(x, 0)) | (b.x & ~bmask(x, 0));
+      out.y = (a.y & bmask(x, 1)) | (b.y & ~bmask(x, 1));
+      out.z = (a.z & bmask(x, 2)) | (b.z & ~bmask(x, 2));
+      out.w = (a.w & bmask(x, 3)) | (b.w & ~bmask(x, 3));
+    }
+    *reinterpret_cast<uint4*>(vd + w) = out;
+  }
+}
+
 int main() {
   const uint64_t n = (1ull << 30) / kEnt;
   uint8_t *s, *kd, *vd, *kd2, *vd2;
@@ -88,20 +121,21 @@ int main() {
   hipEventCreate(&e1);
   const double bytes = 2.0 * n * (kKey + kVal);
   for (int wg : {1024, 2048, 4096, 8192}) {
-    for (int v = 0; v < 2; v++) {
+    for (int v = 0; v < 3; v++) {
       float best = 1e9;
       for (int r = 0; r < 7; r++) {
         hipEventRecord(e0);
         if (v == 0) hipLaunchKernelGGL(pieces, dim3(wg), dim3(256), 0, 0, s, kd, vd, n);
-        else hipLaunchKernelGGL(merged, dim3(wg), dim3(256), 0, 0, s, kd2, vd2, n);
+        else if (v == 1) hipLaunchKernelGGL(merged, dim3(wg), dim3(256), 0, 0, s, kd2, vd2, n);
+        else hipLaunchKernelGGL(merged32, dim3(wg), dim3(256), 0, 0, s, kd2, vd2, (uint32_t)n);
         hipEventRecord(e1);
         hipEventSynchronize(e1);
         float ms;
         hipEventElapsedTime(&ms, e0, e1);
         if (r && ms < best) best = ms;
       }
-      printf("%-7s grid %5d: %.4f ms  %.0f GB/s (read + write of keys and values)\n",
-             v ? "merged" : "pieces", wg, best, bytes / (best / 1e3) / 1e9);
+      printf("%-8s grid %5d: %.4f ms  %.0f GB/s (read + write of keys and values)\n",
+             v == 2 ? "merged32" : v ? "merged" : "pieces", wg, best, bytes / (best / 1e3) / 1e9);
     }
   }
   // both variants wrote the same streams

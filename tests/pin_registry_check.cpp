@@ -107,7 +107,10 @@ int main(int argc, char** argv) {
     R.add(base + 100, 5000, g1);
     M.live.emplace(base + 100, 5000);
     g2 = R.gaps(base + 5200, 9000);
-    CHECK(g2.size() == 1 && g2[0].first == base + 2 * page, "shared page re-pinned");
+    // inward rounding: [base+100, +5000) pins no whole page... [base+5200, +9000) pins pages 2-3
+    CHECK(g1.empty(), "a range without a whole page pinned something");
+    CHECK(g2.size() == 1 && g2[0].first == base + 2 * page && g2[0].second == base + 3 * page,
+          "whole inner pages");
     for (auto& g : g2) M.pin(g);
     R.add(base + 5200, 9000, g2);
     M.live.emplace(base + 5200, 9000);
@@ -131,11 +134,11 @@ int main(int argc, char** argv) {
     CHECK(R.segments() == 0 && R.users() == 0, "leak after the shared-page case");
     // register / unregister / register again at the same address
     for (int k = 0; k < 3; k++) {
-      std::vector<Range> g = R.gaps(base + 64, 3 * page);
-      CHECK(g.size() == 1, "re-register gap count");
+      std::vector<Range> g = R.gaps(base + 64, 4 * page);
+      CHECK(g.size() == 1 && g[0].second - g[0].first == 3 * page, "re-register gap count");
       for (auto& x : g) M.pin(x);
-      R.add(base + 64, 3 * page, g);
-      M.live.emplace(base + 64, 3 * page);
+      R.add(base + 64, 4 * page, g);
+      M.live.emplace(base + 64, 4 * page);
       M.check(R);
       rel.clear();
       rep.clear();
