@@ -420,9 +420,16 @@ def cpu_baseline(torch, w, seconds: float) -> dict:
     reps = max(1, int(seconds / max(t1, 1e-3)))
     secs, _ = oracle_ffi.decode_bench(host, offs, lens, threads, reps)
     gibs = end * reps / secs / (1 << 30)
-    s1, _ = oracle_ffi.decode_bench(host, offs, lens, 1, 1)
-    reps1 = max(1, int(min(5.0, seconds / 2) / max(s1, 1e-3)))
-    secs1, _ = oracle_ffi.decode_bench(host, offs, lens, 1, reps1)
+    # thread scaling (1, 4, 16 threads and every core this job may use), ~3 s each: says whether
+    # the port is bound by cores or by the host's memory bandwidth
+    scaling = {}
+    for t in sorted({1, 4, 16, threads}):
+        if t > threads:
+            continue
+        st, _ = oracle_ffi.decode_bench(host, offs, lens, t, 1)
+        rt = max(1, int(min(3.0, seconds / 4) / max(st, 1e-3)))
+        secs_t, _ = oracle_ffi.decode_bench(host, offs, lens, t, rt)
+        scaling[str(t)] = round(end * rt / secs_t / (1 << 30), 3)
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -436,7 +443,7 @@ def cpu_baseline(torch, w, seconds: float) -> dict:
             "sample": f"{end} B ({nb} blocks) of the same blocks, x{reps} passes, "
                       f"{secs:.1f}s, materialize outputs; C restatement of "
                       f"table/iterator.go:93-135 (oracle/sstref.c)",
-            "single_core_gibs": round(end * reps1 / secs1 / (1 << 30), 3),
+            "single_core_gibs": scaling["1"], "threads_gibs": scaling,
             "host_cpus": cores, "cpu_model": cpu_model}
 
 

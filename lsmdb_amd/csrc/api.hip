@@ -465,10 +465,12 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     // slots; same box: walk 0.2296 -> 0.210 ms, view 0.258 -> 0.233 ms, decode 1,365 -> 1,400
     // GiB/s, profiles/r05c, r05d, r05e).  With every 256-block tile resident the wide tile is
     // slightly slower (walk 0.2005 vs 0.2036 ms).  LSMGPU_WSC_WIDE=0 / 1 forces it off / on.
-    // copy: blocks of <= 63 entries write their key and value streams as aligned 16-B chunks
-    // (copy_stream_aligned); LSMGPU_WSC_ALIGN=0 keeps the unaligned 16-B pieces
+    // copy: LSMGPU_WSC_ALIGN=1 writes the key and value streams of blocks of <= 63 entries as
+    // aligned 16-B chunks (copy_entries_aligned).  Off by default: same-box A/B it is slower
+    // (C2 copy 0.617-0.763 vs 0.495 ms) -- it does not cut the L2 write requests (TCP_TCC_WRITE_REQ
+    // 19.6 M vs 19.9 M per launch) and doubles the VALU / vector-read instructions
     const char* al_env = getenv("LSMGPU_WSC_ALIGN");
-    p.walign = al_env && atoi(al_env) == 0 ? 0u : 1u;
+    p.walign = al_env && atoi(al_env) == 1 ? 1u : 0u;
     const char* ww_env = getenv("LSMGPU_WSC_WIDE");
     const uint64_t cus = (uint64_t)c->num_cus;
     p.wwide = ww_env ? (atoi(ww_env) != 0 ? 576u : 0u)
@@ -514,6 +516,13 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     // d_result is zeroed by the walk kernel when a copy launch follows it (the copy's atomics
     // come after the kernel boundary): one operation fewer per decode.  A view-only decode
     // that ends in the walk updates d_result from every workgroup, so it is zeroed first.
+#ifdef LSMGPU_STAMPS
+    if (getenv("LSMGPU_STAMPS")) {  // diagnostic build: the walk's per-tile stamps (decode_wsc.hip)
+      static DevBuf stamp_buf;
+      HIPC(stamp_buf.ensure((16 + (size_t)nblk * 4) * 8));
+      p.stamps = stamp_buf.as<uint64_t>();
+    }
+#endif
     if (p.wfuse || p.wscopy) HIPC(hipMemsetAsync(d_result, 0, 8 * sizeof(uint64_t), c->stream));
     else p.zero_result = 1;
     if (c->ktime) HIPC(hipEventRecord(c->kev[0], c->stream));

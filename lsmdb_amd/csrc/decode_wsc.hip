@@ -164,6 +164,20 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
 // 266,403 blocks: 1,041 tiles of 256 for 1,024 resident slots, and the 17-tile second wave cost
 // the walk 0.030 ms and the view decode 0.045 ms (same-box A/B, profiles/r05c); 463 tiles of 576
 // are all resident.  WIDE keeps no per-lane tables besides the rows (no s_first / s_off).
+// Diagnostic build only (LSMGPU_BUILD_STAMPS=1, run with LSMGPU_STAMPS=1): per tile, the
+// s_memrealtime (100 MHz) of its start, its walk's end (every wave), its look-back's end and its
+// epilogue's end (wave 0), written to p.stamps[16 + 4 tile ..] and summarized by the host.
+#ifdef LSMGPU_STAMPS
+#define WSC_STAMP(slot, v)                                                                  \
+  do {                                                                                      \
+    if (p.stamps && tid == 0) p.stamps[16 + (uint64_t)tile * 4 + (slot)] = (v);             \
+  } while (0)
+#else
+#define WSC_STAMP(slot, v) \
+  do {                     \
+  } while (0)
+#endif
+
 template <int MODE, uint32_t TB, uint32_t CH = 32, uint32_t SLOT = kStageSlot>  // TB = blocks per tile
 __global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) wsc_walk_kernel(DecodeParams p) {
   constexpr bool WIDE = MODE != kWalkGroup && TB > 256;
@@ -210,6 +224,9 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) ws
   const bool scopy = kWave64 && p.wscopy && !p.wfuse;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t ntiles = (p.nblk + TB - 1) / TB;
+#ifdef LSMGPU_STAMPS
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
   if (tid == 0) {
     const uint32_t t = atomicAdd(p.gcnt, 1u);
     if (t == ntiles - 1) atomicExch(p.gcnt, 0u);  // every ticket is taken
@@ -217,6 +234,9 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) ws
   }
   __syncthreads();
   const uint32_t tile = s_tile;
+#ifdef LSMGPU_STAMPS
+  WSC_STAMP(0, t_start);
+#endif
   // the result block is zeroed by the workgroup holding ticket 0 (see api.hip), before anything
   // else: every other tile's look-back ends only on a record chained to tile 0's, so no flag
   // (the look-back timeout, result[5] |= 2) can be set before this and then erased
@@ -531,6 +551,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) ws
     s_wave[wave][2] = iv;
   }
   __syncthreads();
+  WSC_STAMP(1, __builtin_amdgcn_s_memrealtime());
   if (wave == 0) {
     uint32_t tn = 0, tk = 0, tv = 0;
     for (uint32_t w = 0; w < kWaves; w++) {
@@ -552,6 +573,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) ws
     }
   }
   __syncthreads();
+  WSC_STAMP(2, __builtin_amdgcn_s_memrealtime());
   uint32_t en_b = 0;  // this thread's block's first entry (kWalkLaneView's view loop)
   const uint32_t off_b = MODE != kWalkGroup ? lane_off : 0u;
   if (b < p.nblk) {
@@ -615,6 +637,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) ws
         }
       }
     }
+    WSC_STAMP(3, __builtin_amdgcn_s_memrealtime());
     return;
   }
   if constexpr (KEEP) {
@@ -681,6 +704,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) ws
         emit(f, L);
       }
     }
+    WSC_STAMP(3, __builtin_amdgcn_s_memrealtime());
     return;
   }
   if constexpr (WIDE) return;  // (never launched with the non-kept view epilogue below)
@@ -838,73 +862,167 @@ __device__ __forceinline__ void copy_entries(const DecodeParams& p, const uint32
   }
 }
 
-// One output stream (keys or values) of a block with n <= 63 entries and no prefix-compressed
-// entry, written as ALIGNED 16-B chunks (round 5).  The copy's unaligned, overlapping 16-B pieces
-// reach L2 as ~54-B write requests (19.9 M per C2 1 GiB copy vs 8.4 M 128-B ones for a streaming
-// copy of the same bytes, profiles/r05g); with aligned chunks every store instruction writes whole
-// lines (per-block probe, scripts/align_probe.hip: 0.41-0.44 vs 0.49-0.56 ms).  Stream position u
-// (relative to the block's first byte in the stream, at address B) of entry e comes from block
-// byte src_e + u - so_e; lane e (< n) holds so_e (the entry's stream offset) and src_e, lanes >= n
-// hold so = S (the block's stream length).  Chunk i covers [u0 + 16 i, +16) with B + u0 16-B
-// aligned; its lane finds the last entry e with so_e <= u by a lane-shuffle binary search, loads 16
-// bytes from e's source and merges the bytes of the entries after e (one more load each, in place
-// under byte masks: the load starts k bytes before the next entry's first byte, k = bytes taken so
-// far).  Every load stays inside the block: from e at offset >= 0, from later entries at most 15
-// bytes before their first byte (their header and key precede it), never past a full chunk's
-// last byte.  The <= 15 bytes before u0 and after the last whole chunk share their 16-B chunks with
-// the neighbouring blocks' streams: one lane per byte.
+// Aligned output chunks (round 5).  The copy's unaligned, overlapping 16-B pieces reach L2 as
+// ~54-B write requests (19.9 M per C2 1 GiB copy vs 8.4 M 128-B ones for a streaming copy of the
+// same bytes, profiles/r05g); written as aligned 16-B chunks, every store instruction covers
+// whole lines (per-block probe, scripts/align_probe.hip: 0.41-0.44 vs 0.49-0.56 ms).  A stream
+// (keys or values) of a block starts at address B and holds S bytes; its 16-B grid starts at u0
+// (B + u0 aligned) and has nfull whole chunks [u0 + 16 i, +16) ending at gend.  Entry e holds
+// stream bytes [so_e, so_e1) from block byte src_e on; the lanes of e's group write the chunks
+// that START inside [so_e, so_e1) -- no search, as the pieces do -- loading 16 bytes from e's
+// source and, when the chunk runs into the next entries, 16 more from each, starting k bytes
+// before that entry's first byte (k = bytes taken so far), merged under byte masks.  Loads stay
+// in the block: from e at offset >= 0, from later entries at most 15 bytes before their first
+// byte (their header and key precede it), never past a whole chunk's last byte.  The bytes before
+// u0 and from gend on share their chunks with the neighbouring blocks' streams: one lane a byte.
 __device__ __forceinline__ uint32_t bytes_below(uint32_t k, uint32_t d) {  // mask of dword d's bytes < k
   const int32_t t = (int32_t)k - 4 * (int32_t)d;
   return t >= 4 ? 0xffffffffu : t <= 0 ? 0u : (1u << (8 * t)) - 1u;
 }
-__device__ __forceinline__ void copy_stream_aligned(uint8_t* B, uint32_t S, uint32_t so, uint32_t src,
-                                                    uint32_t n, const uint8_t* blk, uint32_t lane) {
-  if (S == 0) return;
-  const uint32_t u0 = min((uint32_t)((16u - ((uintptr_t)B & 15u)) & 15u), S);
-  const uint32_t nfull = (S - u0) >> 4;
-  auto owner = [&](uint32_t u) -> uint32_t {  // the last entry e < n with so_e <= u (so_0 = 0)
-    uint32_t L = 0;
-#pragma unroll
-    for (uint32_t st = 32; st >= 1; st >>= 1) {
-      const uint32_t cand = L + st;
-      const uint32_t sc = (uint32_t)__shfl((int)so, (int)min(cand, 63u));
-      if (cand < n && sc <= u) L = cand;
-    }
-    return L;
-  };
-  for (uint32_t i0 = 0; i0 < nfull; i0 += kWave) {
-    const bool on = i0 + lane < nfull;
-    const uint32_t u = u0 + 16u * min(i0 + lane, nfull - 1);
-    const uint32_t e = owner(u);
-    const uint32_t so_e = (uint32_t)__shfl((int)so, (int)e), src_e = (uint32_t)__shfl((int)src, (int)e);
-    uint32_t k = (uint32_t)__shfl((int)so, (int)e + 1) - u;  // bytes of the chunk from entry e
-    uint4 w;
-    __builtin_memcpy(&w, blk + src_e + (u - so_e), 16);
-    uint32_t f = e + 1;
-    while (__ballot(on && k < 16u)) {  // entries after e (uniform: every lane shuffles)
-      const uint32_t fc = min(f, 62u);
-      const uint32_t src_f = (uint32_t)__shfl((int)src, (int)fc);
-      const uint32_t so_f1 = (uint32_t)__shfl((int)so, (int)fc + 1);
-      if (on && k < 16u) {
-        uint4 w2;
-        __builtin_memcpy(&w2, blk + src_f - k, 16);
-        w.x = (w.x & bytes_below(k, 0)) | (w2.x & ~bytes_below(k, 0));
-        w.y = (w.y & bytes_below(k, 1)) | (w2.y & ~bytes_below(k, 1));
-        w.z = (w.z & bytes_below(k, 2)) | (w2.z & ~bytes_below(k, 2));
-        w.w = (w.w & bytes_below(k, 3)) | (w2.w & ~bytes_below(k, 3));
-        k = so_f1 - u;
-      }
-      f++;
-    }
-    if (on) *reinterpret_cast<uint4*>(B + u) = w;
+__device__ __forceinline__ uint32_t grid0(const uint8_t* B, uint32_t S) {
+  return min((uint32_t)((16u - ((uintptr_t)B & 15u)) & 15u), S);
+}
+// stream position and source of entry e from its record and the next one (no prefix-compressed
+// entry: the key offset is pos - 10 e - value offset)
+struct StreamPos {
+  uint32_t so, so1, src;
+};
+__device__ __forceinline__ StreamPos stream_pos(bool key, uint32_t e, uint32_t m0, uint32_t m1) {
+  const uint32_t hp = m0 & 0xffffu, vo = m0 >> 16, hp1 = m1 & 0xffffu, vo1 = m1 >> 16;
+  const uint32_t vl = vo1 - vo, kl = hp1 - hp - 10 - vl;
+  if (key) {
+    const uint32_t ko = hp - 10 * e - vo;
+    return StreamPos{ko, ko + kl, hp + 10};
   }
-  // the head [0, u0) and the tail [u0 + 16 nfull, S): one lane per byte
-  const uint32_t ut = u0 + 16u * nfull;
-  const bool hb = lane < 16 ? lane < u0 : (lane < 32 && ut + (lane - 16) < S);
-  const uint32_t q = min(lane < 16 ? lane : ut + (lane - 16), S - 1);
-  const uint32_t e = owner(q);
-  const uint32_t so_e = (uint32_t)__shfl((int)so, (int)e), src_e = (uint32_t)__shfl((int)src, (int)e);
-  if (hb) B[q] = blk[src_e + q - so_e];
+  return StreamPos{vo, vo1, hp + 10 + kl};
+}
+__device__ __forceinline__ uint4 merge_from(uint4 w, uint4 w2, uint32_t k) {  // bytes >= k from w2
+  w.x = (w.x & bytes_below(k, 0)) | (w2.x & ~bytes_below(k, 0));
+  w.y = (w.y & bytes_below(k, 1)) | (w2.y & ~bytes_below(k, 1));
+  w.z = (w.z & bytes_below(k, 2)) | (w2.z & ~bytes_below(k, 2));
+  w.w = (w.w & bytes_below(k, 3)) | (w2.w & ~bytes_below(k, 3));
+  return w;
+}
+// the whole chunk of stream positions [g, g + 16), its first bytes from entry e (records m0, m1;
+// m2 = record e + 2): both loads are issued before either is used; a chunk running past entry
+// e + 1 (entries < 16 B) takes the rest entry by entry
+__device__ __forceinline__ void chunk_out(bool key, uint8_t* B, uint32_t g, uint32_t e, uint32_t m1,
+                                          uint32_t m2, const StreamPos& sp, const uint32_t* meta,
+                                          const uint8_t* blk) {
+  uint4 w;
+  __builtin_memcpy(&w, blk + sp.src + (g - sp.so), 16);
+  uint32_t k = sp.so1 - g;
+  if (k < 16u) {
+    const StreamPos fp = stream_pos(key, e + 1, m1, m2);
+    uint4 w2;
+    __builtin_memcpy(&w2, blk + fp.src - k, 16);
+    w = merge_from(w, w2, k);
+    k = fp.so1 - g;
+    uint32_t f = e + 2, mf = m2;
+    while (k < 16u) {  // rare
+      const uint32_t mf1 = meta[f + 1];
+      const StreamPos hp = stream_pos(key, f, mf, mf1);
+      __builtin_memcpy(&w2, blk + hp.src - k, 16);
+      w = merge_from(w, w2, k);
+      k = hp.so1 - g;
+      f++;
+      mf = mf1;
+    }
+  }
+  *reinterpret_cast<uint4*>(B + g) = w;
+}
+// the chunk starts of [so, so1) on the grid (u0, gend): the first and the count
+__device__ __forceinline__ void chunk_starts(uint32_t so, uint32_t so1, uint32_t u0, uint32_t gend,
+                                             uint32_t& g0, uint32_t& nc) {
+  g0 = so <= u0 ? u0 : u0 + ((so - u0 + 15u) & ~15u);
+  const uint32_t hi = min(so1, gend);
+  nc = g0 < hi ? (hi - g0 + 15u) >> 4 : 0u;
+}
+
+// The bytes of both streams outside their whole chunks (< 16 before u0, < 16 from gend on): lanes
+// 0-15 the key stream's head, 16-31 its tail, 32-47 / 48-63 the value stream's.  The byte is
+// loaded here (before the chunks) and stored by store_edge after them.  Usually the head lies in
+// entry 0 and the tail in entry n - 1 (records from `pre` when n < 64); else the entry is found by
+// stepping through the records.
+struct EdgeByte {
+  uint8_t* dst;
+  uint32_t v;
+};
+__device__ __forceinline__ EdgeByte load_edge(const uint32_t* meta, const uint8_t* blk, uint8_t* kbase,
+                                              uint8_t* vbase, uint32_t n, uint32_t K, uint32_t V,
+                                              uint32_t lane, uint32_t pre) {
+  const bool key = lane < 32, tail = (lane & 16) != 0;
+  // records 0, 1 and n - 1, n (uniform shuffles: every lane takes part)
+  const uint32_t r0 = (uint32_t)__shfl((int)pre, 0), r1 = (uint32_t)__shfl((int)pre, 1);
+  uint32_t rl0, rl1;
+  if (n < kWave) {
+    rl0 = (uint32_t)__shfl((int)pre, (int)n - 1);
+    rl1 = (uint32_t)__shfl((int)pre, (int)n);
+  } else {
+    rl0 = meta[n - 1];
+    rl1 = meta[n];
+  }
+  uint8_t* B = key ? kbase : vbase;
+  const uint32_t S = key ? K : V;
+  if (!B || S == 0) return EdgeByte{nullptr, 0};
+  const uint32_t u0 = grid0(B, S), gend = u0 + ((S - u0) & ~15u);
+  const uint32_t q = tail ? gend + (lane & 15) : (lane & 15);
+  if (tail ? q >= S : q >= u0) return EdgeByte{nullptr, 0};
+  uint32_t e = tail ? n - 1 : 0;
+  StreamPos sp = tail ? stream_pos(key, e, rl0, rl1) : stream_pos(key, 0, r0, r1);
+  if (tail) {
+    while (sp.so > q || sp.so1 <= q) {  // (empty entries: so == so1)
+      e--;
+      sp = stream_pos(key, e, meta[e], meta[e + 1]);
+    }
+  } else {
+    while (sp.so1 <= q) {
+      e++;
+      sp = stream_pos(key, e, meta[e], meta[e + 1]);
+    }
+  }
+  return EdgeByte{B + q, blk[sp.src + (q - sp.so)]};
+}
+
+template <uint32_t J, uint32_t G>
+__device__ __forceinline__ void copy_entries_aligned(const uint32_t* meta, const uint8_t* blk,
+                                                     uint8_t* kbase, uint8_t* vbase, uint32_t n,
+                                                     uint32_t K, uint32_t V, uint32_t sub,
+                                                     uint32_t split, uint32_t lane, uint32_t pre) {
+  const uint32_t j = lane & (J - 1);
+  const EdgeByte eb = load_edge(meta, blk, kbase, vbase, n, K, V, lane, pre);
+  const uint32_t ku0 = kbase ? grid0(kbase, K) : 0u, vu0 = vbase ? grid0(vbase, V) : 0u;
+  const uint32_t kend = kbase ? ku0 + ((K - ku0) & ~15u) : 0u;  // no key chunks without kbase
+  const uint32_t vend = vbase ? vu0 + ((V - vu0) & ~15u) : 0u;
+  for (uint32_t e0 = sub * G * (kWave / J); e0 < n; e0 += split * G * (kWave / J)) {
+    // records e, e + 1, e + 2 by lane shuffle while e + 2 < 64 (`pre` holds records 0 .. 63)
+    const bool shuffled = e0 + G * (kWave / J) + 1 < kWave;
+#pragma unroll 1
+    for (int i = 0; i < (int)G; i++) {
+      const uint32_t e = e0 + i * (kWave / J) + (lane / J);
+      const uint32_t ec = min(e, n - 1);
+      uint32_t m0, m1, m2;
+      if (shuffled) {
+        m0 = (uint32_t)__shfl((int)pre, (int)ec);
+        m1 = (uint32_t)__shfl((int)pre, (int)ec + 1);
+        m2 = (uint32_t)__shfl((int)pre, (int)min(ec + 2, n));
+      } else {
+        m0 = meta[ec];
+        m1 = meta[ec + 1];
+        m2 = meta[min(ec + 2, n)];
+      }
+      if (e >= n) continue;
+      const StreamPos kp = stream_pos(true, e, m0, m1), vp = stream_pos(false, e, m0, m1);
+      uint32_t kg, nkc, vg, nvc;
+      chunk_starts(kp.so, kp.so1, ku0, kend, kg, nkc);
+      chunk_starts(vp.so, vp.so1, vu0, vend, vg, nvc);
+      for (uint32_t q = j; q < nkc + nvc; q += J) {
+        if (q < nkc) chunk_out(true, kbase, kg + 16 * q, e, m1, m2, kp, meta, blk);
+        else chunk_out(false, vbase, vg + 16 * (q - nkc), e, m1, m2, vp, meta, blk);
+      }
+    }
+  }
+  if (eb.dst) *eb.dst = (uint8_t)eb.v;
 }
 
 // A block with prefix-compressed entries (plen > 0: never written by Builder; the
@@ -1000,17 +1118,13 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
   // (round 4: each lane's first piece of every entry of a pass loaded before any store left
   // the copy unchanged, 0.6038 vs 0.6042 ms, profiles/r04c; compiled into this kernel it also
   // raised the VGPRs from 44 to 90, 8 -> 5 waves per SIMD: removed)
-  if (p.walign && mat && split == 1 && n < kWave) {
-    // aligned output chunks (copy_stream_aligned): records 0 .. n sit one per lane in `pre`
+  if (p.walign && mat && split == 1) {
+    // aligned output chunks + the stream edges byte by byte (copy_entries_aligned)
     entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
-    const uint32_t m1 = (uint32_t)__shfl((int)pre, (int)min(lane + 1, kWave - 1));
-    const uint32_t hp = pre & 0xffffu, vo = pre >> 16, hp1 = m1 & 0xffffu, vo1 = m1 >> 16;
-    const uint32_t vl = vo1 - vo, kl = hp1 - hp - 10 - vl;
-    const bool ent = lane < n;
-    if (kbase)
-      copy_stream_aligned(kbase, K, ent ? hp - 10 * lane - vo : K, hp + 10, n, blk, lane);
-    if (vbase)
-      copy_stream_aligned(vbase, V, ent ? vo : V, hp + 10 + kl, n, blk, lane);
+    if (p.wj == 16 || (p.wj == 0 && avg > 128))
+      copy_entries_aligned<16, 2>(meta, blk, kbase, vbase, n, K, V, sub, split, lane, pre);
+    else
+      copy_entries_aligned<8, 5>(meta, blk, kbase, vbase, n, K, V, sub, split, lane, pre);
   } else if (p.wj == 16 || (p.wj == 0 && avg > 128)) {
     copy_entries<16, 2, true>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
   } else {
@@ -1076,6 +1190,48 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
   else
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 256>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
   hipError_t e = hipGetLastError();
+#ifdef LSMGPU_STAMPS
+  if (e == hipSuccess && p.stamps) {  // diagnostics: the walk's per-tile timeline
+    const uint32_t tb = p.wwalk == kWalkGroup ? 256 / p.wlanes
+                      : (p.wwide ? p.wwide : (p.wfuse && p.wkeep && p.wtile == 192) || p.wtile == 192 ? 192 : 256);
+    const uint32_t nt = (nblk + tb - 1) / tb;
+    std::vector<uint64_t> h((size_t)nt * 4);
+    (void)hipMemcpyAsync(h.data(), p.stamps + 16, h.size() * 8, hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
+    uint64_t t0 = ~0ull, t1 = 0;
+    double walk = 0, look = 0, epi = 0;
+    std::vector<double> starts, ends;
+    for (uint32_t t = 0; t < nt; t++) {
+      const uint64_t* r = &h[4 * (size_t)t];
+      t0 = std::min(t0, r[0]);
+      t1 = std::max(t1, r[3]);
+      walk += (double)(r[1] - r[0]);
+      look += (double)(r[2] - r[1]);
+      epi += (double)(r[3] - r[2]);
+    }
+    for (uint32_t t = 0; t < nt; t++) {
+      starts.push_back((h[4 * (size_t)t] - t0) / 100.0);
+      ends.push_back((h[4 * (size_t)t + 3] - t0) / 100.0);
+    }
+    std::sort(starts.begin(), starts.end());
+    std::sort(ends.begin(), ends.end());
+    auto pct = [](const std::vector<double>& v, double q) { return v[(size_t)(q * (v.size() - 1))]; };
+    fprintf(stderr, "[lsmgpu] walk stamps (us, %u tiles of %u): span %.2f | per tile: walk %.2f, scan + "
+            "look-back %.2f, epilogue %.2f | starts p50 %.2f p90 %.2f max %.2f | ends p10 %.2f p50 %.2f "
+            "p90 %.2f max %.2f\n", nt, tb, (t1 - t0) / 100.0, walk / nt / 100.0, look / nt / 100.0,
+            epi / nt / 100.0, pct(starts, 0.5), pct(starts, 0.9), starts.back(), pct(ends, 0.1),
+            pct(ends, 0.5), pct(ends, 0.9), ends.back());
+    if (const char* f = getenv("LSMGPU_STAMPS_FILE")) {
+      if (FILE* o = fopen(f, "a")) {
+        for (uint32_t t = 0; t < nt; t++)
+          fprintf(o, "%u %llu %llu %llu %llu\n", t, (unsigned long long)(h[4 * (size_t)t] - t0),
+                  (unsigned long long)(h[4 * (size_t)t + 1] - t0), (unsigned long long)(h[4 * (size_t)t + 2] - t0),
+                  (unsigned long long)(h[4 * (size_t)t + 3] - t0));
+        fclose(o);
+      }
+    }
+  }
+#endif
   if (e == hipSuccess && mid) e = hipEventRecord(mid, s);
   // view-only, or the staged walk copying its blocks: the walk wrote everything
   if (e != hipSuccess || p.wfuse || p.wscopy) return e;

@@ -8,6 +8,9 @@
 //            chunks, one lane each, bytes from one or two entries (two unaligned loads merged
 //            under byte masks)
 //   aligned_pf: the same with every load of the block issued before its first store
+//   dense  : unaligned 16-B pieces as the pieces variant writes them (each inside its entry, the
+//            last overlapping back), but packed one per lane: 64 consecutive value pieces per
+//            store instruction (keys one lane each) -- density without alignment
 // (merge_store_probe.hip's merged variant fetched every input line twice: keys and values were
 // handled in separate passes of its grid-stride loop.)
 // Build: hipcc --offload-arch=gfx950 -O3 -o scripts/align_probe scripts/align_probe.hip
@@ -105,6 +108,22 @@ __global__ void __launch_bounds__(256) aligned(const uint8_t* __restrict__ s, ui
   }
 }
 
+__global__ void __launch_bounds__(256) dense(const uint8_t* __restrict__ s, uint8_t* __restrict__ kd,
+                                             uint8_t* __restrict__ vd, uint32_t nb) {
+  const uint32_t lane = threadIdx.x & 63, w0 = (blockIdx.x * 256 + threadIdx.x) >> 6, nw = gridDim.x * 4;
+  constexpr uint32_t kPieces = (kVal + 15) / 16;  // 7 per value
+  for (uint32_t b = w0; b < nb; b += nw) {
+    const uint8_t* bs = s + (uint64_t)b * kPer * kEnt;
+    if (lane < kPer)
+      st16(kd + ((uint64_t)b * kPer + lane) * kKey, ld16(bs + lane * kEnt + 10));
+    for (uint32_t c = lane; c < kPer * kPieces; c += 64) {
+      const uint32_t e = c / kPieces, j = c - e * kPieces;
+      const uint32_t o = min(16u * j, kVal - 16);
+      st16(vd + ((uint64_t)b * kPer + e) * kVal + o, ld16(bs + e * kEnt + 10 + kKey + o));
+    }
+  }
+}
+
 int main() {
   const uint32_t nb = (uint32_t)((1ull << 30) / (kPer * kEnt));
   const uint64_t n = (uint64_t)nb * kPer;
@@ -121,15 +140,16 @@ int main() {
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   const double bytes = 2.0 * n * (kKey + kVal);
-  const char* names[] = {"pieces", "aligned", "aligned_pf"};
+  const char* names[] = {"pieces", "aligned", "aligned_pf", "dense"};
   for (int wg : {1024, 2048, 4096, 8192}) {
-    for (int v = 0; v < 3; v++) {
+    for (int v = 0; v < 4; v++) {
       float best = 1e9;
       for (int r = 0; r < 7; r++) {
         (void)hipEventRecord(e0);
         if (v == 0) hipLaunchKernelGGL(pieces, dim3(wg), dim3(256), 0, 0, s, kd, vd, nb);
         else if (v == 1) hipLaunchKernelGGL(aligned<false>, dim3(wg), dim3(256), 0, 0, s, kd2, vd2, nb);
-        else hipLaunchKernelGGL(aligned<true>, dim3(wg), dim3(256), 0, 0, s, kd2, vd2, nb);
+        else if (v == 2) hipLaunchKernelGGL(aligned<true>, dim3(wg), dim3(256), 0, 0, s, kd2, vd2, nb);
+        else hipLaunchKernelGGL(dense, dim3(wg), dim3(256), 0, 0, s, kd2, vd2, nb);
         (void)hipEventRecord(e1);
         (void)hipEventSynchronize(e1);
         float ms;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 same-box A/B: the copy's aligned 16-B output chunks (LSMGPU_WSC_ALIGN, default on) vs
+# Round-5 same-box A/B: the copy's aligned 16-B output chunks (LSMGPU_WSC_ALIGN=1, default off) vs
 # the unaligned pieces, alternating, two rounds, on the given config.
 # Usage (on the GPU box): bash scripts/r05_align_ab.sh <tag> [config] [GiB]
 set -o pipefail

@@ -1,18 +1,15 @@
 """One lsmgpu_ctx per OS thread, several threads at once (include/lsmgpu.h: "one lsmgpu_ctx per
 OS thread"; the cgo shim's model, and compactBuildTables' per-table goroutines,
 levels.go:281-298).  Two host threads, each with its own Codec on device 0, decode different
-shards -- a large batch (walk-scan-copy / one-pass), a small one (100 blocks) -- and run a whole
+shards -- a large batch (the lane walk + copy), a small one (100 blocks: the group walk) -- and run a whole
 compaction at the same time, several rounds; every output is checked against the oracle.
 ctypes drops the GIL inside each library call, so the threads' HIP work really overlaps."""
 import threading
 
-import numpy as np
 import pytest
 
-from lsmdb_amd import workload
 from lsmdb_amd.codec import Codec
 
-import open_cases as C
 from test_gpu_parity import _assert_same, _cols, _sst_blocks
 from test_gpu_shim import _bottom_run, _oracle_compaction, _tables
 
@@ -59,4 +56,3 @@ def test_two_contexts_concurrently(oracle, monkeypatch, path):
         t.join(timeout=110)
     assert not any(t.is_alive() for t in threads), "a worker thread did not finish"
     assert not errors, errors
-    _ = (np, workload, C)
