@@ -466,11 +466,12 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     // GiB/s, profiles/r05c, r05d, r05e).  With every 256-block tile resident the wide tile is
     // slightly slower (walk 0.2005 vs 0.2036 ms).  LSMGPU_WSC_WIDE=0 / 1 forces it off / on.
     // copy: LSMGPU_WSC_ALIGN=1 writes the key and value streams of blocks of <= 63 entries as
-    // aligned 16-B chunks (copy_entries_aligned).  Off by default: same-box A/B it is slower
+    // aligned 16-B chunks per entry group (copy_entries_aligned), =2 as dense aligned chunks over
+    // both streams (copy_chunks).  Off by default: same-box A/B, =1 is slower
     // (C2 copy 0.617-0.763 vs 0.495 ms) -- it does not cut the L2 write requests (TCP_TCC_WRITE_REQ
     // 19.6 M vs 19.9 M per launch) and doubles the VALU / vector-read instructions
     const char* al_env = getenv("LSMGPU_WSC_ALIGN");
-    p.walign = al_env && atoi(al_env) == 1 ? 1u : 0u;
+    p.walign = al_env ? (uint32_t)atoi(al_env) : 0u;  // 2: dense aligned chunks (copy_chunks)
     const char* ww_env = getenv("LSMGPU_WSC_WIDE");
     const uint64_t cus = (uint64_t)c->num_cus;
     p.wwide = ww_env ? (atoi(ww_env) != 0 ? 576u : 0u)

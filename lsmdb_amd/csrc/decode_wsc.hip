@@ -137,7 +137,7 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
                                            uint32_t pre, uint32_t n, uint32_t K, uint32_t V,
                                            uint32_t sw, uint64_t en, uint64_t ek, uint64_t ev,
                                            uint32_t off, uint32_t sub, uint32_t split,
-                                           uint32_t lane, const Src& src);
+                                           uint32_t lane, const Src& src, uint32_t* tab = nullptr);
 
 // K1: lane = block; a workgroup = a tile of 256 consecutive blocks, tiles taken in ticket order
 // (p.gcnt[0]).  After the walk the workgroup scans its blocks' {entries, key bytes, value
@@ -1025,6 +1025,108 @@ __device__ __forceinline__ void copy_entries_aligned(const uint32_t* meta, const
   if (eb.dst) *eb.dst = (uint8_t)eb.v;
 }
 
+// Dense aligned output chunks (LSMGPU_WSC_ALIGN=2, blocks of <= 63 entries whose two streams
+// span <= kChunkOwn chunks): the key and value streams of the block as ALIGNED 16-B chunks over
+// one combined chunk index (key chunks, then value chunks), 64 consecutive chunks per store
+// instruction.  Each entry lane publishes its stream ends and input bases in LDS and marks the
+// chunks whose first byte it holds (an LDS owner table); a chunk lane loads 16 B from its owner
+// and 16 more from each following entry it runs into, merged under byte masks (input byte of
+// stream byte x in entry e: D_e + x, so a later entry's load starts < 16 B before its first
+// byte: its own header / key, inside the block).  A stream's partial head and tail chunks
+// (shared with the neighbouring blocks' streams) are stored as naturally aligned 8/4/2/1-B parts.
+constexpr uint32_t kChunkOwn = 512;  // owner-table bytes per wave
+constexpr uint32_t kChunkLds = 4 * 64 + kChunkOwn / 4;  // u32 per wave: so1 / D per stream + owners
+
+__device__ __forceinline__ uint32_t bytes_from(uint32_t k, uint32_t d) {  // dword d's bytes >= k
+  const int32_t t = (int32_t)k - 4 * (int32_t)d;
+  return t <= 0 ? 0xffffffffu : t >= 4 ? 0u : ~((1u << (8 * t)) - 1u);
+}
+// 16 bytes at block byte q; past `lim` (the readable end) bytes are zero (the batch's last block)
+__device__ __forceinline__ uint4 load16_lim(const uint8_t* blk, uint32_t q, uint32_t lim) {
+  uint4 v;
+  if (q + 16 <= lim) {
+    __builtin_memcpy(&v, blk + q, 16);
+  } else {
+    v = make_uint4(0, 0, 0, 0);
+    for (uint32_t i = 0; i < 16 && q + i < lim; i++) set_byte(v, (int)i, blk[q + i]);
+  }
+  return v;
+}
+// the first len (< 16) bytes of v at d as naturally aligned 8/4/2/1-B stores
+__device__ __forceinline__ void store_head(uint8_t* d, uint4 v, uint32_t len) {
+  uint32_t s = 0;
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  while (len) {
+    const uintptr_t a = (uintptr_t)d;
+    uint32_t sz = 8;
+    while (sz > len || (a & (sz - 1))) sz >>= 1;
+    uint64_t x = 0;
+    for (uint32_t i = 0; i < sz; i++)
+      x |= (uint64_t)((w[(s + i) >> 2] >> (8 * ((s + i) & 3))) & 0xffu) << (8 * i);
+    if (sz == 8) *reinterpret_cast<uint64_t*>(d) = x;
+    else if (sz == 4) *reinterpret_cast<uint32_t*>(d) = (uint32_t)x;
+    else if (sz == 2) *reinterpret_cast<uint16_t*>(d) = (uint16_t)x;
+    else *d = (uint8_t)x;
+    d += sz;
+    s += sz;
+    len -= sz;
+  }
+}
+__device__ __forceinline__ bool chunks_fit(const uint8_t* kbase, const uint8_t* vbase, uint32_t K, uint32_t V) {
+  const uint32_t ak = (uint32_t)((uintptr_t)kbase & 15u), av = (uint32_t)((uintptr_t)vbase & 15u);
+  return (kbase ? (K + ak + 15) >> 4 : 0u) + (vbase ? (V + av + 15) >> 4 : 0u) <= kChunkOwn;
+}
+__device__ __forceinline__ void copy_chunks(const uint8_t* blk, uint32_t lim, uint8_t* kbase,
+                                            uint8_t* vbase, uint32_t n, uint32_t K, uint32_t V,
+                                            uint32_t lane, uint32_t pre, uint32_t* tab) {
+  uint32_t* const so1 = tab;            // [2][64]: key / value stream end of entry e
+  uint32_t* const dd = tab + 128;       // [2][64]: input base D_e of each stream
+  uint8_t* const own = reinterpret_cast<uint8_t*>(tab + 256);
+  const uint32_t ak = kbase ? (uint32_t)((uintptr_t)kbase & 15u) : 0u;
+  const uint32_t av = vbase ? (uint32_t)((uintptr_t)vbase & 15u) : 0u;
+  const uint32_t CK = kbase ? (K + ak + 15) >> 4 : 0u, CV = vbase ? (V + av + 15) >> 4 : 0u;
+  const uint32_t m0 = pre, m1 = (uint32_t)__shfl((int)pre, (int)min(lane + 1, kWave - 1));
+  const uint32_t hp = m0 & 0xffffu, vo = m0 >> 16, hp1 = m1 & 0xffffu, vo1 = m1 >> 16;
+  const uint32_t vl = vo1 - vo, kl = hp1 - hp - 10 - vl, ko = hp - 10 * lane - vo, ko1 = ko + kl;
+  if (lane < n) {
+    so1[lane] = ko1;
+    dd[lane] = hp + 10 - ko;
+    so1[64 + lane] = vo1;
+    dd[64 + lane] = hp1 - vo1;
+    // chunk c >= 1 of a stream starts at stream byte 16 c - a, chunk 0 at byte 0
+    if (CK) {
+      const uint32_t lo = ko == 0 ? 0u : (ko + ak + 15) >> 4, hi = kl ? (ko1 + ak + 15) >> 4 : lo;
+      for (uint32_t c = lo; c < hi; c++) own[c] = (uint8_t)lane;
+    }
+    if (CV) {
+      const uint32_t lo = vo == 0 ? 0u : (vo + av + 15) >> 4, hi = vl ? (vo1 + av + 15) >> 4 : lo;
+      for (uint32_t c = lo; c < hi; c++) own[CK + c] = (uint8_t)lane;
+    }
+  }
+  wave_lds_fence();
+  for (uint32_t c = lane; c < CK + CV; c += kWave) {
+    const bool key = c < CK;
+    const uint32_t cc = key ? c : c - CK, a = key ? ak : av, S = key ? K : V, s = key ? 0u : 64u;
+    const uint32_t x0 = cc ? 16 * cc - a : 0u;           // the chunk's first stream byte
+    const uint32_t L = min(cc ? 16u : 16u - a, S - x0);  // and its byte count
+    uint32_t e = own[c];
+    uint4 v = load16_lim(blk, dd[s + e] + x0, lim);
+    uint32_t k = so1[s + e] - x0;
+    while (k < L) {  // the chunk runs into entry e + 1
+      e++;
+      const uint4 w = load16_lim(blk, dd[s + e] + x0, lim);
+      v.x = (v.x & ~bytes_from(k, 0)) | (w.x & bytes_from(k, 0));
+      v.y = (v.y & ~bytes_from(k, 1)) | (w.y & bytes_from(k, 1));
+      v.z = (v.z & ~bytes_from(k, 2)) | (w.z & bytes_from(k, 2));
+      v.w = (v.w & ~bytes_from(k, 3)) | (w.w & bytes_from(k, 3));
+      k = so1[s + e] - x0;
+    }
+    uint8_t* d = (key ? kbase : vbase) + x0;
+    if (L == 16) *reinterpret_cast<uint4*>(d) = v;
+    else store_head(d, v, L);
+  }
+}
+
 // A block with prefix-compressed entries (plen > 0: never written by Builder; the
 // format the iterator accepts): entries 64 at a time, lane = entry, plen read from the header,
 // key offsets by a wave scan of plen + stored key bytes; keys bytewise as baseKey[:plen] ++ diff
@@ -1069,7 +1171,7 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
                                            uint32_t pre, uint32_t n, uint32_t K, uint32_t V,
                                            uint32_t sw, uint64_t en, uint64_t ek, uint64_t ev,
                                            uint32_t off, uint32_t sub, uint32_t split,
-                                           uint32_t lane, const Src& src) {
+                                           uint32_t lane, const Src& src, uint32_t* tab) {
   const uint32_t st = sw & ~kPlenFlag;
   if (lane == 0 && sub == 0) {
     if (p.blk_first) p.blk_first[b] = (uint32_t)en;
@@ -1118,7 +1220,12 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
   // (round 4: each lane's first piece of every entry of a pass loaded before any store left
   // the copy unchanged, 0.6038 vs 0.6042 ms, profiles/r04c; compiled into this kernel it also
   // raised the VGPRs from 44 to 90, 8 -> 5 waves per SIMD: removed)
-  if (p.walign && mat && split == 1) {
+  if (p.walign == 2 && mat && split == 1 && n < kWave && tab && chunks_fit(kbase, vbase, K, V)) {
+    // dense aligned chunks over both streams (copy_chunks)
+    entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
+    const uint64_t lim = p.data_len - off;
+    copy_chunks(blk, lim < 0xffffffffull ? (uint32_t)lim : 0xffffffffu, kbase, vbase, n, K, V, lane, pre, tab);
+  } else if (p.walign == 1 && mat && split == 1) {
     // aligned output chunks + the stream edges byte by byte (copy_entries_aligned)
     entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
     if (p.wj == 16 || (p.wj == 0 && avg > 128))
@@ -1153,7 +1260,9 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   const uint64_t* bs = p.wbase + 3ull * b;
   const uint64_t en = uniform64(bs[0]), ek = uniform64(bs[1]), ev = uniform64(bs[2]);
   const uint32_t off = uniform(p.blk_off[b]);
-  copy_block(p, b, meta, pre, n, K, V, sw, en, ek, ev, off, sub, split, lane, GlobalBytes{p.data + off});
+  __shared__ uint32_t s_chunk[4][kChunkLds];  // copy_chunks' per-wave tables
+  copy_block(p, b, meta, pre, n, K, V, sw, en, ek, ev, off, sub, split, lane, GlobalBytes{p.data + off},
+             s_chunk[threadIdx.x >> 6]);
 }
 
 

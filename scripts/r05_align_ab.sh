@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-5 same-box A/B: the copy's aligned 16-B output chunks (LSMGPU_WSC_ALIGN=1, default off) vs
-# the unaligned pieces, alternating, two rounds, on the given config.
-# Usage (on the GPU box): bash scripts/r05_align_ab.sh <tag> [config] [GiB]
+# Round-5 same-box A/B of the copy's store patterns (LSMGPU_WSC_ALIGN: 0 the unaligned pieces,
+# the default; 1 aligned chunks per entry group; 2 dense aligned chunks), alternating, two rounds.
+# Usage (on the GPU box): bash scripts/r05_align_ab.sh <tag> [config] [GiB] [modes, e.g. "0 2"]
 set -o pipefail
-T=${1:-r05align}; CFG=${2:-2}; GIB=${3:-1.0}
+T=${1:-r05align}; CFG=${2:-2}; GIB=${3:-1.0}; MODES=${4:-"0 2"}
 O=gpurun_out/$T
 mkdir -p $O
 line() {
@@ -23,6 +23,5 @@ run() {  # name env...
   line $name $O/bench_$name.json
 }
 for r in 1 2; do
-  run align_$r LSMGPU_WSC_ALIGN=1
-  run pieces_$r LSMGPU_WSC_ALIGN=0
+  for m in $MODES; do run align${m}_$r LSMGPU_WSC_ALIGN=$m; done
 done
