@@ -472,6 +472,14 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     // 19.6 M vs 19.9 M per launch) and doubles the VALU / vector-read instructions
     const char* al_env = getenv("LSMGPU_WSC_ALIGN");
     p.walign = al_env ? (uint32_t)atoi(al_env) : 0u;  // 2: dense aligned chunks (copy_chunks)
+    // tile prefixes: every thread of the workgroup sums some predecessors' aggregates
+    // (lookback_partial; same box: C2 walk 0.2085-0.2086 vs 0.2091-0.2106 ms, C4 decode
+    // 0.0676-0.0679 vs 0.0686-0.0689 ms, profiles/r05t); LSMGPU_WSC_LOOKBACK=window keeps the
+    // windowed decoupled look-back
+    const char* lb_env = getenv("LSMGPU_WSC_LOOKBACK");
+    p.wlbfull = lb_env && strcmp(lb_env, "window") == 0 ? 0u : 1u;
+    const char* pad_env = getenv("LSMGPU_WSC_PADLDS");  // experiments only: fewer tiles per CU
+    p.wpad = pad_env ? (uint32_t)atoi(pad_env) : 0u;
     const char* ww_env = getenv("LSMGPU_WSC_WIDE");
     const uint64_t cus = (uint64_t)c->num_cus;
     p.wwide = ww_env ? (atoi(ww_env) != 0 ? 576u : 0u)

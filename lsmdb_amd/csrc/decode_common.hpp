@@ -192,6 +192,34 @@ __device__ inline Tot lookback(const uint64_t* rec, uint32_t g, uint64_t tag, ui
   return ex;
 }
 
+// Look-back by every thread of the workgroup (round 5, the default; LSMGPU_WSC_LOOKBACK=window
+// selects the windowed one above): thread i sums
+// the AGGREGATES of predecessor tiles i, i + nthreads, ... (waiting for each to be published),
+// so the exclusive prefix costs about one round trip however many tiles finish together --
+// the windowed look-back above walks back 64 tiles per round trip while no inclusive prefix is
+// published yet (1,041 tiles finishing at once: ~35 us, profiles/r05q).  Returns this thread's
+// partial sums; the caller reduces them over the workgroup.  A timeout sets result[5] bit 2.
+__device__ inline Tot lookback_partial(const uint64_t* rec, uint32_t g, uint64_t tag, uint32_t tid,
+                                       uint32_t nthreads, uint64_t* result) {
+  Tot s{0, 0, 0};
+  for (uint32_t j = tid; j < g; j += nthreads) {
+    const uint64_t* r = rec + (uint64_t)j * 8;
+    uint32_t a, b, c;
+    SpinBound bound;
+    while (!read3(r, tag, a, b, c)) {
+      if (bound.expired()) {
+        atomicOr(reinterpret_cast<unsigned long long*>(result + 5), 2ull);
+        return s;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+    s.n = sat_add(s.n, a);
+    s.k = sat_add(s.k, b);
+    s.v = sat_add(s.v, c);
+  }
+  return s;
+}
+
 // ------------------------------------------------------------------------ LDS-DMA staging
 typedef __attribute__((address_space(3))) void lds_void_t;
 // One LDS-DMA piece: lane l's 16 bytes at gptr -> LDS lds + 16 * l (global_load_lds_dwordx4,

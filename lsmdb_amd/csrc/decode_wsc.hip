@@ -137,7 +137,8 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
                                            uint32_t pre, uint32_t n, uint32_t K, uint32_t V,
                                            uint32_t sw, uint64_t en, uint64_t ek, uint64_t ev,
                                            uint32_t off, uint32_t sub, uint32_t split,
-                                           uint32_t lane, const Src& src, uint32_t* tab = nullptr);
+                                           uint32_t lane, const Src& src, uint32_t* tab = nullptr,
+                                           bool duties = true);
 
 // K1: lane = block; a workgroup = a tile of 256 consecutive blocks, tiles taken in ticket order
 // (p.gcnt[0]).  After the walk the workgroup scans its blocks' {entries, key bytes, value
@@ -212,6 +213,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) ws
   __shared__ uint32_t s_tile;
   __shared__ uint32_t s_wave[kWaves][3];
   __shared__ uint32_t s_ex[3];
+  __shared__ uint32_t s_part[kWaves][3];  // p.wlbfull: each wave's share of the predecessors' sums
   __shared__ uint32_t s_first[KEEP || WIDE ? 1 : kThreads + 1];  // p.wfuse: tile-relative first entry
   // each block's input offset (group walks; the lane walk's non-kept view epilogue)
   __shared__ uint32_t s_off[MODE == kWalkGroup ? TB : (KEEP || WIDE ? 1 : kThreads)];
@@ -552,7 +554,39 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) ws
   }
   __syncthreads();
   WSC_STAMP(1, __builtin_amdgcn_s_memrealtime());
-  if (wave == 0) {
+  if (p.wlbfull) {
+    // every tile publishes its aggregate; every thread sums some predecessors' (lookback_partial)
+    uint32_t tn = 0, tk = 0, tv = 0;
+    for (uint32_t w = 0; w < kWaves; w++) {
+      tn = sat_add(tn, s_wave[w][0]);
+      tk = sat_add(tk, s_wave[w][1]);
+      tv = sat_add(tv, s_wave[w][2]);
+    }
+    uint64_t* R = p.lb + (uint64_t)tile * 8;
+    if (wave == 0) store3(R, p.tag, tn, tk, tv, lane);
+    Tot part{0, 0, 0};
+    if (tile > 0 && !(p.ablate & 1)) part = lookback_partial(p.lb, tile, p.tag, tid, kThreads, p.result);
+    const uint32_t pn = wave_sum_sat(part.n), pk = wave_sum_sat(part.k), pv = wave_sum_sat(part.v);
+    if (lane == 0) {
+      s_part[wave][0] = pn;
+      s_part[wave][1] = pk;
+      s_part[wave][2] = pv;
+    }
+    __syncthreads();
+    if (wave == 0) {
+      Tot ex{0, 0, 0};
+      for (uint32_t w = 0; w < kWaves; w++) {
+        ex.n = sat_add(ex.n, s_part[w][0]);
+        ex.k = sat_add(ex.k, s_part[w][1]);
+        ex.v = sat_add(ex.v, s_part[w][2]);
+      }
+      if (lane == 0) {
+        s_ex[0] = ex.n;
+        s_ex[1] = ex.k;
+        s_ex[2] = ex.v;
+      }
+    }
+  } else if (wave == 0) {
     uint32_t tn = 0, tk = 0, tv = 0;
     for (uint32_t w = 0; w < kWaves; w++) {
       tn = sat_add(tn, s_wave[w][0]);
@@ -590,12 +624,17 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) ws
       s_cb[0][tid] = en;
       s_cb[1][tid] = ek;
       s_cb[2][tid] = ev;
-    } else if (!p.wfuse) {
-      uint64_t* bs = p.wbase + 3ull * b;
-      bs[0] = en;
-      bs[1] = ek;
-      bs[2] = ev;
-    } else {  // view-only decode: the copy kernel's per-block duties, done here
+    } else {
+      if (!p.wfuse) {  // the copy kernel's bases
+        uint64_t* bs = p.wbase + 3ull * b;
+        bs[0] = en;
+        bs[1] = ek;
+        bs[2] = ev;
+      }
+      // The per-block outputs, here for every decode (round 5; view-only decodes have no copy):
+      // one thread per block writes consecutive words -- from the copy kernel, one lane per
+      // block, they were scattered 4-B stores into lines shared by workgroups on other XCDs
+      // (C2 copy 0.50 -> 0.465 ms without them, profiles/r05s)
       if (p.blk_first) p.blk_first[b] = en;
       if (p.blk_status) p.blk_status[b] = (int32_t)st;
       if (st != LSMGPU_BLK_OK) {
@@ -609,8 +648,13 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) ws
         p.result[1] = (uint64_t)ek + K;
         p.result[2] = (uint64_t)ev + V;
       }
-      if (!((uint64_t)en + n <= p.ent_cap && (uint64_t)en + n <= 0xffffffffull))
-        atomicOr(reinterpret_cast<unsigned long long*>(p.result + 5), 1ull);
+      bool fits = (uint64_t)en + n <= p.ent_cap && (uint64_t)en + n <= 0xffffffffull;
+      if (!p.wfuse && (p.mode & LSMGPU_MODE_MATERIALIZE)) {  // the copy's output streams
+        const uint64_t kend = (uint64_t)ek + K, vend = (uint64_t)ev + V;
+        fits = fits && (kend <= p.key_cap || !p.key_data) && (vend <= p.val_cap || !p.val_data) &&
+               kend < 0xffffffffull && vend <= 0xffffffffull;
+      }
+      if (!fits) atomicOr(reinterpret_cast<unsigned long long*>(p.result + 5), 1ull);
     }
   }
   if (!p.wfuse) {
@@ -1171,9 +1215,11 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
                                            uint32_t pre, uint32_t n, uint32_t K, uint32_t V,
                                            uint32_t sw, uint64_t en, uint64_t ek, uint64_t ev,
                                            uint32_t off, uint32_t sub, uint32_t split,
-                                           uint32_t lane, const Src& src, uint32_t* tab) {
+                                           uint32_t lane, const Src& src, uint32_t* tab,
+                                           bool duties) {
   const uint32_t st = sw & ~kPlenFlag;
-  if (lane == 0 && sub == 0) {
+  // duties: the per-block outputs, unless the walk kernel wrote them (every copy launch)
+  if (duties && lane == 0 && sub == 0 && !(p.ablate & 32)) {  // (timing-only ablation 32)
     if (p.blk_first) p.blk_first[b] = (uint32_t)en;
     if (p.blk_status) p.blk_status[b] = (int32_t)st;
     if (st != LSMGPU_BLK_OK) {
@@ -1197,7 +1243,7 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
     ok = ok && kend < 0xffffffffull && vend <= 0xffffffffull;
   }
   if (!ok) {
-    if (lane == 0 && sub == 0) atomicOr(reinterpret_cast<unsigned long long*>(p.result + 5), 1ull);
+    if (duties && lane == 0 && sub == 0) atomicOr(reinterpret_cast<unsigned long long*>(p.result + 5), 1ull);
     return;
   }
   if (n == 0 || (p.ablate & 2)) return;
@@ -1235,8 +1281,9 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
   } else if (p.wj == 16 || (p.wj == 0 && avg > 128)) {
     copy_entries<16, 2, true>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
   } else {
-    entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
-    if (mat)
+    // (timing-only ablations: 8 no per-entry outputs, 16 no pieces)
+    if (!(p.ablate & 8)) entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
+    if (mat && !(p.ablate & 16))
       copy_entries<8, 5, false>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
   }
 }
@@ -1262,7 +1309,7 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   const uint32_t off = uniform(p.blk_off[b]);
   __shared__ uint32_t s_chunk[4][kChunkLds];  // copy_chunks' per-wave tables
   copy_block(p, b, meta, pre, n, K, V, sw, en, ek, ev, off, sub, split, lane, GlobalBytes{p.data + off},
-             s_chunk[threadIdx.x >> 6]);
+             s_chunk[threadIdx.x >> 6], false);
 }
 
 
@@ -1296,7 +1343,11 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 256, 16>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
   else if (p.wtile == 192)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 192>), dim3((nblk + 191) / 192), dim3(192), 0, s, p);
-  else
+  else if (p.wpad) {  // (residency experiments: unused dynamic LDS limits the tiles per CU)
+    (void)hipFuncSetAttribute((const void*)wsc_walk_kernel<kWalkLane, 256>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.wpad);
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 256>), dim3((nblk + 255) / 256), dim3(256), p.wpad, s, p);
+  } else
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 256>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
   hipError_t e = hipGetLastError();
 #ifdef LSMGPU_STAMPS

@@ -55,6 +55,8 @@ struct DecodeParams {
   uint32_t wtile;           // lane walks: blocks (= threads) per workgroup, 192 or 256
   uint32_t walign;          // copy: aligned 16-B output chunks for blocks of <= 63 entries
   uint32_t wwide;           // lane walks: 0 (256-block tiles, 4 per CU) or 576 (2 per CU)
+  uint32_t wlbfull;         // walk: every thread of a tile sums predecessor aggregates (no windows)
+  uint32_t wpad;            // lane walk (256-block tiles): dynamic LDS bytes (residency experiments)
   uint32_t wscopy;          // 64-lane staged group walk: each wave copies its block from LDS
   uint32_t wslot;           // 64-lane staged group walk: 0 = kStageSlot, 1 = kStageSlotSmall
   uint32_t wsub;            // group walk: odd-shaped entries re-guessed inside a round

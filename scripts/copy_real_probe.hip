@@ -59,14 +59,34 @@ struct Blocks {
   uint8_t* kd;
   uint8_t* vd;
   uint32_t nb;
+  const uint32_t* en;    // first entry of the block
+  uint32_t* key_end;     // per-entry end offsets (EO variants)
+  uint32_t* val_end;
 };
 
+// EO: the per-entry end offsets first, one lane per entry (entry_outputs); XCD: workgroup w runs
+// on XCD w % 8 (round-robin dispatch), so each XCD takes a contiguous eighth of the blocks
+template <bool EO, bool XCD>
 __global__ void __launch_bounds__(256) pieces(Blocks p) {
-  const uint32_t lane = threadIdx.x & 63, b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t wg = blockIdx.x;
+  if (XCD) {
+    const uint32_t per = gridDim.x / 8;  // grid a multiple of 8
+    wg = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  }
+  const uint32_t b = wg * 4 + (threadIdx.x >> 6);
   if (b >= p.nb) return;
   const uint32_t n = p.n[b];
   const uint32_t* meta = p.rec + (uint64_t)b * kCap;
   const uint32_t pre = meta[lane];
+  if (EO) {
+    const uint32_t m1 = (uint32_t)__shfl((int)pre, (int)min(lane + 1, 63u));
+    const uint32_t vo1 = m1 >> 16;
+    if (lane < n) {
+      p.key_end[p.en[b] + lane] = (uint32_t)(p.ek[b] + (m1 & 0xffffu) - 10 * (lane + 1) - vo1);
+      p.val_end[p.en[b] + lane] = (uint32_t)(p.ev[b] + vo1);
+    }
+  }
   const uint8_t* blk = p.data + p.off[b];
   uint8_t* kb = p.kd + p.ek[b];
   uint8_t* vb = p.vd + p.ev[b];
@@ -191,7 +211,7 @@ int main() {
   // byte target), a 13-B terminator after each block
   srand(7);
   std::vector<uint8_t> data;
-  std::vector<uint32_t> off, nn, rec, KK, VV;
+  std::vector<uint32_t> off, nn, rec, KK, VV, ens;
   std::vector<uint64_t> ek, ev;
   const uint64_t target = 1ull << 30;
   uint64_t kt = 0, vt = 0;
@@ -215,6 +235,7 @@ int main() {
     r.resize(kCap, 0);
     data.insert(data.end(), blk.begin(), blk.end());
     off.push_back(o);
+    ens.push_back((uint32_t)(kt / 16));
     nn.push_back(n);
     rec.insert(rec.end(), r.begin(), r.end());
     KK.push_back(16 * n);
@@ -237,7 +258,7 @@ int main() {
     }
   }
   uint8_t *d_data, *kd, *vd;
-  uint32_t *d_off, *d_n, *d_rec, *d_K, *d_V;
+  uint32_t *d_off, *d_n, *d_rec, *d_K, *d_V, *d_en, *d_ke, *d_ve;
   uint64_t *d_ek, *d_ev;
   (void)hipMalloc(&d_data, data.size() + 64);
   (void)hipMalloc(&kd, kt + 64);
@@ -249,6 +270,10 @@ int main() {
   (void)hipMalloc(&d_rec, rec.size() * 4);
   (void)hipMalloc(&d_ek, nb * 8);
   (void)hipMalloc(&d_ev, nb * 8);
+  (void)hipMalloc(&d_en, nb * 4);
+  (void)hipMalloc(&d_ke, kt / 16 * 4 + 64);
+  (void)hipMalloc(&d_ve, kt / 16 * 4 + 64);
+  (void)hipMemcpy(d_en, ens.data(), nb * 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(d_data, data.data(), data.size(), hipMemcpyHostToDevice);
   (void)hipMemcpy(d_off, off.data(), nb * 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(d_n, nn.data(), nb * 4, hipMemcpyHostToDevice);
@@ -257,24 +282,28 @@ int main() {
   (void)hipMemcpy(d_rec, rec.data(), rec.size() * 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(d_ek, ek.data(), nb * 8, hipMemcpyHostToDevice);
   (void)hipMemcpy(d_ev, ev.data(), nb * 8, hipMemcpyHostToDevice);
-  Blocks p{d_data, d_off, d_n, d_rec, d_ek, d_ev, d_K, d_V, kd, vd, nb};
+  Blocks p{d_data, d_off, d_n, d_rec, d_ek, d_ev, d_K, d_V, kd, vd, nb, d_en, d_ke, d_ve};
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   printf("%u blocks, %zu B input, %llu key + %llu value bytes\n", nb, data.size(),
          (unsigned long long)kt, (unsigned long long)vt);
   const double bytes = (double)(kt + vt) * 2;
-  const char* names[] = {"pieces", "chunks"};
+  const char* names[] = {"pieces", "chunks", "pieces_eo", "pieces_eo_xcd", "pieces_xcd"};
+  const uint32_t grid = (nb + 31) / 32 * 8;  // a multiple of 8 workgroups
   uint64_t bad_all = 0;
   for (int round = 0; round < 2; round++) {
-    for (int v = 0; v < 2; v++) {
+    for (int v = 0; v < 5; v++) {
       (void)hipMemset(kd, 0, kt);
       (void)hipMemset(vd, 0, vt);
       float best = 1e9, sum = 0;
       for (int r = 0; r < 11; r++) {
         (void)hipEventRecord(e0);
-        if (v == 0) hipLaunchKernelGGL(pieces, dim3((nb + 3) / 4), dim3(256), 0, 0, p);
-        else hipLaunchKernelGGL(chunks, dim3((nb + 3) / 4), dim3(256), 0, 0, p);
+        if (v == 0) hipLaunchKernelGGL((pieces<false, false>), dim3(grid), dim3(256), 0, 0, p);
+        else if (v == 1) hipLaunchKernelGGL(chunks, dim3(grid), dim3(256), 0, 0, p);
+        else if (v == 2) hipLaunchKernelGGL((pieces<true, false>), dim3(grid), dim3(256), 0, 0, p);
+        else if (v == 3) hipLaunchKernelGGL((pieces<true, true>), dim3(grid), dim3(256), 0, 0, p);
+        else hipLaunchKernelGGL((pieces<false, true>), dim3(grid), dim3(256), 0, 0, p);
         (void)hipEventRecord(e1);
         (void)hipEventSynchronize(e1);
         float ms;
@@ -291,7 +320,7 @@ int main() {
       for (uint64_t i = 0; i < kt; i++) bad += k2[i] != kref[i];
       for (uint64_t i = 0; i < vt; i++) bad += v2[i] != vref[i];
       bad_all += bad;
-      printf("%-7s best %.4f ms mean %.4f ms  %.0f GB/s  mismatching bytes %llu\n", names[v], best, sum / 10,
+      printf("%-13s best %.4f ms mean %.4f ms  %.0f GB/s  mismatching bytes %llu\n", names[v], best, sum / 10,
              bytes / (best / 1e3) / 1e9, (unsigned long long)bad);
     }
   }

@@ -449,13 +449,16 @@ def test_prefix_compressed_large_output(codec, oracle, monkeypatch, path):
     _assert_same(codec.decode_host(data, off, ln), ref, f"path={path}")
 
 
-@pytest.mark.parametrize("chunk", ["32", "16"])
-def test_wsc_many_tiles(codec, oracle, monkeypatch, chunk):
+@pytest.mark.parametrize("chunk,lookback", [("32", "window"), ("16", "window"), ("32", "full"),
+                                            ("16", "full")])  # (full: the default)
+def test_wsc_many_tiles(codec, oracle, monkeypatch, chunk, lookback):
     """The walk kernel's tiles (256 blocks, ticket order) find their output bases by decoupled
     look-back over ~40 tile records: C2 blocks plus a ragged last tile, checked against the
     oracle on every output array, three launches back to back (the ticket reset); 32- and
-    16-record flush chunks."""
+    16-record flush chunks; the windowed look-back and the workgroup-wide sum of every
+    predecessor's aggregate (LSMGPU_WSC_LOOKBACK=full)."""
     monkeypatch.setenv("LSMGPU_WSC_CHUNK", chunk)
+    monkeypatch.setenv("LSMGPU_WSC_LOOKBACK", lookback)
     c = _cols(2, 330000, seed=13)
     sst, _, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, 0, 4096)
     sst = sst + b"{}" + (2).to_bytes(4, "big")
@@ -507,7 +510,7 @@ def test_wsc_lanes_per_entry(codec, oracle, monkeypatch, lanes):
 @pytest.mark.parametrize("walk", ["lane", "lane16", "lane192", "lane576", "lane_flush", "lane_viewsearch", "group", "group2",
                                   "group4", "group16", "group32", "group64", "group64_copy", "group64s",
                                   "group64g", "group64g_copy", "group_sub", "group16_sub",
-                                  "group_dpp"])
+                                  "group_dpp", "lane_lbwin", "lane576_lbwin", "group_lbwin"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     """Walk-scan-copy's walks (LSMGPU_WSC_WALK): one lane per block from HBM, or 8 / 4
@@ -518,6 +521,9 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     tile and a block ending at the buffer's end (plus C5 32 KiB blocks for the HBM walks)."""
     from lsmdb_amd.codec import MODE_MATERIALIZE, MODE_VIEW
     monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
+    if walk.endswith("_lbwin"):  # the windowed decoupled look-back (LSMGPU_WSC_LOOKBACK=window)
+        monkeypatch.setenv("LSMGPU_WSC_LOOKBACK", "window")
+        walk = walk[:-len("_lbwin")]
     if walk == "lane16":  # the lane walk flushing 16-record (64-B) chunks
         monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
         monkeypatch.setenv("LSMGPU_WSC_CHUNK", "16")
