@@ -478,6 +478,12 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     // windowed decoupled look-back
     const char* lb_env = getenv("LSMGPU_WSC_LOOKBACK");
     p.wlbfull = lb_env && strcmp(lb_env, "window") == 0 ? 0u : 1u;
+    // group walks (<= 64 blocks per CU, e.g. one 64 MiB table): 8 lanes per block forward plus 8
+    // walking backward from the terminator in other waves (kWalkGroupBi; same box, C4: walk
+    // 0.0402-0.0411 -> 0.0341-0.0354 ms, decode 0.0676-0.0688 -> 0.0614-0.0626 ms, profiles/r05z,
+    // r05aa; 16 + 16 lanes: 0.0378-0.0381).  LSMGPU_WSC_BIDIR=0 / 1 / 2: off / 8 + 8 / 16 + 16
+    const char* bi_env = getenv("LSMGPU_WSC_BIDIR");
+    p.wbidir = bi_env ? (uint32_t)std::min(std::max(atoi(bi_env), 0), 2) : 1u;
     const char* pad_env = getenv("LSMGPU_WSC_PADLDS");  // experiments only: fewer tiles per CU
     p.wpad = pad_env ? (uint32_t)atoi(pad_env) : 0u;
     const char* ww_env = getenv("LSMGPU_WSC_WIDE");
@@ -530,6 +536,7 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
       static DevBuf stamp_buf;
       HIPC(stamp_buf.ensure((16 + (size_t)nblk * 4) * 8));
       p.stamps = stamp_buf.as<uint64_t>();
+      HIPC(hipMemsetAsync(p.stamps, 0, 16 * sizeof(uint64_t), c->stream));  // walk counters
     }
 #endif
     if (p.wfuse || p.wscopy) HIPC(hipMemsetAsync(d_result, 0, 8 * sizeof(uint64_t), c->stream));

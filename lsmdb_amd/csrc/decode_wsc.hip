@@ -100,6 +100,227 @@ __device__ __forceinline__ void flush_meta(uint32_t* dst, const uint32_t* row, u
   }
 }
 
+// kWalkGroupBi (LSMGPU_WSC_BIDIR=1, round 5): the group walk plus a BACKWARD walk of each block,
+// in other waves of the workgroup, from the terminator finishBlock writes (builder.go:121-123:
+// header {0, 0, 3, prev = the last entry}) over the headers' prev fields (builder.go:95-109),
+// so each block's dependent chain is about halved (C4: 23.3 -> 12.4 rounds per block on
+// average, 46 -> 25 at most, profiles/r05y).  Waves 0-1 walk 16 blocks forward, 8 lanes each,
+// exactly as the group walk; waves 2-3 walk the same blocks backward.  They meet through LDS
+// (BiState): the backward waves push each accepted entry (pos | vlen << 16) on the block's
+// stack, then publish the stack depth and the lowest entry B; the forward walk accepts only
+// entries starting below the B it last read.  A backward entry is accepted only as the forward
+// walk would take it: it starts at or above the forward position, has plen 0 and klen > 0, and
+// ends exactly where the entry after it starts (the first at the terminator; a guessed one,
+// bnext - k * stride, by having the guessed shape).  Once the forward position reaches B it must
+// be one of the stacked starts -- then the chains are one (the forward walk from there would
+// step through exactly the stacked entries and stop at the terminator) and the stacked entries
+// above it become records in forward order; if it is not, the chains disagree and the forward
+// walk goes on alone.  (Round 4 ran both directions in the same lanes, and a first round-5
+// version in the same wave in lockstep: the rounds halved but each cost twice as much.)
+struct BiState {
+  uint32_t B;     // lowest published backward entry start (kBiNone: none)
+  uint32_t bn;    // entries on the stack (stack[0] the highest)
+  uint32_t pos;   // the forward position
+  uint32_t done;  // the forward walk has finished, or gone on alone: the backward walk stops
+};
+constexpr uint32_t kBiNone = 0xffffffffu, kBiCap = 64;
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t* a) {
+  return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(uint32_t* a, uint32_t v) {
+  __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <uint32_t L>
+__device__ __forceinline__ void bidir_bwd(const uint8_t* blk, uint32_t len, uint32_t* bst,
+                                          BiState* st, uint32_t k, uint32_t gb) {
+  constexpr uint64_t kMask = (1ull << L) - 1;
+  if (len < 23) return;
+  uint32_t tp, tk, tv;
+  read_hdr(blk + (len - 13), tp, tk, tv);
+  uint32_t bnext;
+  __builtin_memcpy(&bnext, blk + (len - 13) + 6, 4);
+  bnext = __builtin_bswap32(bnext);
+  if ((tp | tk) != 0 || bnext >= len - 13) return;
+  uint32_t B = len - 13, bn = 0, bkref = kBiNone, bvref = 0, bstride = 0;
+  for (;;) {
+    if (lds_ld(&st->done)) break;
+    const uint32_t posf = lds_ld(&st->pos);
+    if (B <= posf) break;  // the forward walk is here already
+    const bool act = (uint64_t)k * bstride <= bnext;
+    const uint32_t q = bnext - k * bstride;
+    uint32_t plen = 1, klen = 0, vlen = 0, prv = kBiNone;
+    if (act && q + 10 <= len) {
+      uint2 w;
+      __builtin_memcpy(&w, blk + q, 8);
+      uint16_t lo;
+      __builtin_memcpy(&lo, blk + q + 8, 2);
+      plen = __builtin_amdgcn_perm(0u, w.x, 0x0c0c0001u);
+      klen = __builtin_amdgcn_perm(0u, w.x, 0x0c0c0203u);
+      vlen = __builtin_amdgcn_perm(0u, w.y, 0x0c0c0001u);
+      prv = (__builtin_amdgcn_perm(0u, w.y, 0x0c0c0203u) << 16) | bswap16(lo);
+    }
+    const uint32_t endq = q + 10 + klen + vlen;
+    const bool ok = act && q + 10 <= len && q >= posf && plen == 0 && klen != 0 &&
+                    (k == 0 ? endq == B : (klen == bkref && vlen == bvref));
+    const uint64_t bb = (__ballot(ok) >> gb) & kMask;
+    uint32_t cnt = bb == kMask ? L : (uint32_t)__builtin_ctzll(~bb);
+    if (bn + cnt > kBiCap) cnt = kBiCap - bn;
+    if (cnt == 0) break;
+    const uint32_t src = gb + cnt - 1;
+    const uint32_t lc = (uint32_t)__shfl((int)q, (int)src), nx = (uint32_t)__shfl((int)prv, (int)src);
+    const uint32_t sh0 = (uint32_t)__shfl((int)(klen | (vlen << 16)), (int)gb);
+    if (k < cnt) bst[bn + k] = q | (vlen << 16);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the entries before the depth
+    bn += cnt;
+    if (k == 0) lds_st(&st->bn, bn);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the depth before B
+    B = lc;
+    if (k == 0) lds_st(&st->B, B);
+    if (cnt == 1) {  // the guessed shape: lane 0's, unless a run of the old one followed it
+      bkref = sh0 & 0xffffu;
+      bvref = sh0 >> 16;
+      bstride = 10 + bkref + bvref;
+    }
+    bnext = nx;
+    if (bn == kBiCap || bnext >= lc) break;
+  }
+}
+
+template <uint32_t L>
+__device__ __forceinline__ void bidir_fwd(const DecodeParams& p, const uint8_t* blk, uint32_t len,
+                                          uint32_t* meta, uint32_t* row, const uint32_t* bst,
+                                          BiState* st, uint32_t k, uint32_t gb, uint32_t& pos,
+                                          uint32_t& gn, uint32_t& gK, uint32_t& gV, uint32_t& gst) {
+  constexpr uint64_t kMask = (1ull << L) - 1;
+  constexpr uint32_t kGroupProbe = 16;
+  uint32_t kref = kBiNone, vref = 0, stride = 0, rounds = 0, depth = 0;
+  bool alone = false, met = false;
+  for (;;) {
+    uint32_t Bc = alone ? kBiNone : lds_ld(&st->B);
+    if (Bc != kBiNone && pos >= Bc) {
+      // the forward position must be one of the stacked starts (stack[0] the highest)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      const uint32_t nb = lds_ld(&st->bn);
+      uint32_t hit = kBiNone;
+      for (uint32_t i = k; i < nb; i += L)
+        if ((bst[i] & 0xffffu) == pos) hit = i;
+      const uint64_t hm = (__ballot(hit != kBiNone) >> gb) & kMask;
+      if (hm) {
+        depth = (uint32_t)__shfl((int)hit, (int)(gb + __builtin_ctzll(hm))) + 1;
+        met = true;
+        break;
+      }
+      alone = true;  // the chains disagree: the forward walk alone from here
+      if (k == 0) lds_st(&st->done, 1);
+      Bc = kBiNone;
+    }
+    const uint32_t q = pos + k * stride;
+    uint32_t plen = 1, klen = 0, vlen = 0;
+    if (q + 10 <= len) read_hdr(blk + q, plen, klen, vlen);
+    const uint32_t endq = q + 10 + klen + vlen;
+    const bool fast = (klen != 0) & (plen == 0) & (endq <= len) & (q < Bc);
+    const bool same = fast & (klen == kref) & (vlen == vref);
+    const uint64_t fb = (__ballot(fast) >> gb) & kMask, sb = (__ballot(same) >> gb) & kMask;
+    if (!(fb & 1)) break;  // entry n needs the general loop (or the block ended)
+    const uint32_t t = sb == kMask ? L : (uint32_t)__builtin_ctzll(~sb);
+    const uint32_t m = t + ((t < L && ((fb >> t) & 1u)) ? 1u : 0u);
+    const uint32_t rec = q | ((gV + k * vref) << 16);
+    const uint32_t idx = gn + k, cend = (gn | 31u) + 1;
+    const bool acc = k < m;
+    if (acc && idx < cend) row[idx & 31] = rec;
+    const uint32_t src = gb + m - 1;
+    pos = (uint32_t)__shfl((int)endq, (int)src);
+    const uint32_t shape = (uint32_t)__shfl((int)(klen | (vlen << 16)), (int)src);
+    if (k == 0) lds_st(&st->pos, pos);
+    gK += t * kref + (m > t ? (shape & 0xffffu) : 0u);
+    gV += t * vref + (m > t ? (shape >> 16) : 0u);
+    gn += m;
+    if (t == 0) {
+      kref = shape & 0xffffu;
+      vref = shape >> 16;
+      stride = 10 + kref + vref;
+    }
+    rounds++;
+    if (gn >= cend) {  // chunk [cend - 32, cend) complete: one full 128-B line
+      __builtin_amdgcn_wave_barrier();
+      reinterpret_cast<uint4*>(meta + cend - 32)[k] =
+          make_uint4(row[4 * k], row[4 * k + 1], row[4 * k + 2], row[4 * k + 3]);
+      __builtin_amdgcn_wave_barrier();  // the chunk is read before the next one fills
+      if (acc && idx >= cend) row[idx & 31] = rec;
+    }
+    if (rounds >= kGroupProbe && 4 * gn < 5 * rounds && lds_ld(&st->bn) < 8) break;
+  }
+  if (k == 0) lds_st(&st->done, 1);
+#ifdef LSMGPU_STAMPS
+  if (p.stamps && k == 0) {  // diagnostics: forward rounds per block, blocks whose chains met
+    atomicAdd(reinterpret_cast<unsigned long long*>(p.stamps + 8), (unsigned long long)rounds);
+    atomicMax(reinterpret_cast<unsigned long long*>(p.stamps + 9), (unsigned long long)rounds);
+    atomicAdd(reinterpret_cast<unsigned long long*>(p.stamps + 10), 1ull);
+    atomicAdd(reinterpret_cast<unsigned long long*>(p.stamps + 11), met ? 1ull : 0ull);
+  }
+#endif
+  if (met) {
+    // the stacked entries stack[depth - 1] (at pos) .. stack[0] in forward order, L per trip
+    // through the record ring: value offsets by a scan of their value lengths, key lengths from
+    // the next entry's start (stack[i - 1], the terminator above stack[0])
+    for (uint32_t i0 = 0; i0 < depth; i0 += L) {
+      const uint32_t i = i0 + k;
+      const bool on = i < depth;
+      const uint32_t si = depth - 1 - i;
+      const uint32_t sv = on ? bst[si] : 0u;
+      const uint32_t nxt = on ? (si ? (bst[si - 1] & 0xffffu) : len - 13) : 0u;
+      const uint32_t pe = sv & 0xffffu, vl = sv >> 16;
+      const uint32_t kl = on ? nxt - pe - 10 - vl : 0u;
+      uint32_t x = vl, y = kl;  // inclusive scans over the group
+#pragma unroll
+      for (uint32_t d = 1; d < L; d <<= 1) {
+        const uint32_t xv = (uint32_t)__shfl_up((int)x, d, L), yv = (uint32_t)__shfl_up((int)y, d, L);
+        if (k >= d) {
+          x += xv;
+          y += yv;
+        }
+      }
+      const uint32_t rec = pe | ((gV + x - vl) << 16);
+      const uint32_t mc = min(L, depth - i0);
+      const uint32_t idx = gn + k, cend = (gn | 31u) + 1;
+      if (on && idx < cend) row[idx & 31] = rec;
+      gV += (uint32_t)__shfl((int)x, (int)(gb + mc - 1));
+      gK += (uint32_t)__shfl((int)y, (int)(gb + mc - 1));
+      gn += mc;
+      if (gn >= cend) {
+        __builtin_amdgcn_wave_barrier();
+        reinterpret_cast<uint4*>(meta + cend - 32)[k] =
+            make_uint4(row[4 * k], row[4 * k + 1], row[4 * k + 2], row[4 * k + 3]);
+        __builtin_amdgcn_wave_barrier();
+        if (on && idx >= cend) row[idx & 31] = rec;
+      }
+    }
+    pos = len - 13;  // at the terminator, where the forward walk stops (iterator.go:124-127)
+    return;
+  }
+  if (k == 0) {  // general loop: every stop rule in the iterator's order (as the group walk)
+    for (;;) {
+      if (pos >= len) break;                                   // iterator.go:115-118
+      if (len - pos < 10) { gst = LSMGPU_BLK_TRUNC_HEADER; break; }
+      uint32_t plen, klen, vlen;
+      read_hdr(blk + pos, plen, klen, vlen);                   // iterator.go:121
+      if ((klen | plen) == 0) break;                           // iterator.go:124-127
+      if (gn == 0 && plen != 0) { gst = LSMGPU_BLK_FIRST_PLEN; break; }  // :129-133
+      if (10 + plen > len) { gst = LSMGPU_BLK_PREFIX_OOB; break; }
+      const uint32_t end = pos + 10 + klen + vlen;             // iterator.go:101-109
+      if (end > len) { gst = LSMGPU_BLK_VALUE_OVERFLOW; break; }
+      row[gn & 31] = pos | (gV << 16);
+      if ((gn & 31) == 31) flush_meta(meta + (gn - 31), row, 32);
+      gK += plen + klen;
+      gV += vlen;
+      gn++;
+      pos = end;
+    }
+  }
+  (void)p;
+}
+
 // Where the copy reads a block's bytes: global memory (the copy kernel), or the walk's LDS slot
 // holding the block at byte sh (the 64-lane staged walk copying its own block, p.wscopy).
 // piece(dst, s0, len, q) = copy_piece16(dst, block + s0, len, q).
@@ -180,13 +401,17 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
 #endif
 
 template <int MODE, uint32_t TB, uint32_t CH = 32, uint32_t SLOT = kStageSlot>  // TB = blocks per tile
-__global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) wsc_walk_kernel(DecodeParams p) {
-  constexpr bool WIDE = MODE != kWalkGroup && TB > 256;
+__global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || TB <= 256 ? 256 : TB)
+    wsc_walk_kernel(DecodeParams p) {
+  // group walks: kWalkGroup, or kWalkGroupBi (a second lane group per block walks backward)
+  constexpr bool GW = MODE == kWalkGroup || MODE == kWalkGroupBi;
+  constexpr bool BI = MODE == kWalkGroupBi;
+  constexpr bool WIDE = !GW && TB > 256;
   static_assert(TB <= 256 || (WIDE && TB <= 1024 && CH == 32), "one thread per block of the tile");
   static_assert(CH == 16 || CH == 32, "16 or 32 records per chunk");
   constexpr bool KEEP = MODE == kWalkLaneView;
   // lane walks: one thread per block, TB = 192, 256 or 576 threads; the group walk: 256 threads
-  constexpr uint32_t kThreads = MODE == kWalkGroup ? 256 : TB;
+  constexpr uint32_t kThreads = GW ? 256 : TB;
   constexpr uint32_t kWaves = kThreads / 64;
   static_assert(kThreads % 64 == 0, "whole waves");
   // LDS row per lane: CH records (+ 1 pad, bank spread), or kViewRec kept records (+ 1; WIDE:
@@ -205,8 +430,8 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) ws
   constexpr uint32_t kSlot = kStaged ? SLOT : 0u;
   static_assert(SLOT % 16 == 0, "16-B chunks (0: no staging)");
   constexpr uint32_t kLdsBytes =
-      MODE == kWalkGroup ? TB * 32 * sizeof(uint32_t) + TB * kSlot : kStageBytes;
-  static_assert(MODE == kWalkGroup || kLdsBytes == kStageBytes,
+      GW ? TB * 32 * sizeof(uint32_t) + TB * kSlot : kStageBytes;
+  static_assert(GW || kLdsBytes == kStageBytes,
                 "the lane walk stages its records per lane");
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   uint32_t* const stage = reinterpret_cast<uint32_t*>(lds);
@@ -216,8 +441,12 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) ws
   __shared__ uint32_t s_part[kWaves][3];  // p.wlbfull: each wave's share of the predecessors' sums
   __shared__ uint32_t s_first[KEEP || WIDE ? 1 : kThreads + 1];  // p.wfuse: tile-relative first entry
   // each block's input offset (group walks; the lane walk's non-kept view epilogue)
-  __shared__ uint32_t s_off[MODE == kWalkGroup ? TB : (KEEP || WIDE ? 1 : kThreads)];
-  constexpr uint32_t kRes = MODE == kWalkGroup ? TB : 1;
+  __shared__ uint32_t s_off[GW ? TB : (KEEP || WIDE ? 1 : kThreads)];
+  constexpr uint32_t kRes = GW ? TB : 1;
+  // kWalkGroupBi: each block's backward-walked entries (pos | vlen << 16), lowest last, and
+  // the state the forward and backward waves share
+  __shared__ uint32_t s_bstack[BI ? TB : 1][BI ? kBiCap : 1];
+  __shared__ BiState s_bi[BI ? TB : 1];
   __shared__ uint32_t s_res[4][kRes];  // group / wave walk: n, K, V, status per block
   __shared__ uint32_t s_stg[kRes];  // group walk: the block is in its LDS slot (kStaged)
   __shared__ uint32_t s_cb[3][kWave64 ? TB : 1];  // p.wscopy: each block's output bases
@@ -248,17 +477,27 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) ws
   const uint32_t b = tid < TB ? tile * TB + tid : 0xffffffffu;
   uint32_t n = 0, K = 0, V = 0, st = LSMGPU_BLK_OK;
   uint32_t lane_off = 0;  // lane walks: this thread's block offset
-  if constexpr (MODE == kWalkGroup) {
+  if constexpr (GW) {
     // L lanes per block: each round the group reads the headers at pos + k * stride (stride =
     // the last accepted entry's size) and accepts the leading run whose guesses were right --
     // lane k is entry n + k iff entries n .. n + k - 1 all had the previous entry's shape.  The
     // guessed lines belong to the next entries of the same block (no extra traffic), the group
     // fetches neighbouring lines together, and the dependent chain shrinks by the run length.
-    constexpr uint32_t L = 256 / TB;
+    // (kWalkGroupBi: waves 0-1 walk the tile's 16 blocks forward, 8 lanes each, as below; waves
+    // 2-3 the same blocks backward: bidir_fwd / bidir_bwd)
+    constexpr uint32_t L = BI ? 128 / TB : 256 / TB;  // lanes per block (per direction)
+    constexpr uint32_t LB = L;
+    static_assert((BI ? 2 : 1) * L * TB == 256, "one tile of blocks per 256-thread workgroup");
     static_assert(L >= 2 && L <= 64 && (L & (L - 1)) == 0, "2..64 lanes per block");
     constexpr uint64_t kMask = L == 64 ? ~0ull : (1ull << (L & 63)) - 1;
     constexpr uint32_t kGroupProbe = 16;
-    const uint32_t g = tid / L, k = tid & (L - 1), gb = lane & ~(L - 1);
+    const uint32_t g = BI ? (tid & 127) / L : tid / L, k = tid & (L - 1), gb = lane & ~(L - 1);
+    const uint32_t kk = k;
+    const bool bw = BI && tid >= 128;  // a backward lane (waves 2-3)
+    if constexpr (BI) {
+      if (tid < TB) s_bi[tid] = BiState{kBiNone, 0u, 0u, 0u};
+      __syncthreads();
+    }
     const uint32_t bg = tile * TB + g;
     uint32_t* row = stage + g * 32;  // the block's current 32-record chunk (one 128-B line)
     if (bg < p.nblk) {
@@ -307,6 +546,10 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) ws
             wave_lds_fence();
           }
         }
+        if constexpr (BI) {
+          if (bw) bidir_bwd<L>(blk, len, s_bstack[g], &s_bi[g], k, gb);
+          else bidir_fwd<L>(p, blk, len, meta, row, s_bstack[g], &s_bi[g], k, gb, pos, gn, gK, gV, gst);
+        } else {
         uint32_t kref = 0xffffffffu, vref = 0, stride = 0;  // no shape yet: round 1 takes one
         uint32_t rounds = 0;
         // p.wsub: a round is a window of L entries; after an odd-shaped entry only the lanes
@@ -391,6 +634,13 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) ws
           // time (C4 shapes, simulated: 2 per round after 8 rounds gives up on 13 % of blocks)
           if (rounds >= kGroupProbe && 4 * gn < 5 * rounds) break;
         }
+#ifdef LSMGPU_STAMPS
+        if (p.stamps && k == 0) {  // diagnostics: rounds per block
+          atomicAdd(reinterpret_cast<unsigned long long*>(p.stamps + 8), (unsigned long long)rounds);
+          atomicMax(reinterpret_cast<unsigned long long*>(p.stamps + 9), (unsigned long long)rounds);
+          atomicAdd(reinterpret_cast<unsigned long long*>(p.stamps + 10), 1ull);
+        }
+#endif
         if (k == 0) {  // general loop: every stop rule in the iterator's order (as the lane walk)
           for (;;) {
             if (pos >= len) break;                                   // iterator.go:115-118
@@ -411,16 +661,19 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) ws
             pos = end;
           }
         }
+        }  // !BI
       }
       // the last chunk (the sentinel last) as whole 16-B parts of its 128-B line, by the group's
       // L lanes (the general loop ran in lane 0: its count is the group's)
-      if (k == 0) row[gn & 31] = pos | (gV << 16);  // sentinel
-      const uint32_t gnl = (uint32_t)__shfl((int)gn, (int)gb);
+      if (!bw) {  // (kWalkGroupBi: the forward lanes hold the block's results)
+      const uint32_t gbl = lane & ~(LB - 1);  // the block's first lane (forward lane 0)
+      if (kk == 0) row[gn & 31] = pos | (gV << 16);  // sentinel
+      const uint32_t gnl = (uint32_t)__shfl((int)gn, (int)gbl);
       wave_lds_fence();
-      for (uint32_t i = k; i < 8; i += L)
+      for (uint32_t i = kk; i < 8; i += LB)
         reinterpret_cast<uint4*>(meta + (gnl & ~31u))[i] =
             make_uint4(row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3]);
-      if (k == 0) {
+      if (kk == 0) {
         s_res[0][g] = gn;
         s_res[1][g] = gK;
         s_res[2][g] = gV;
@@ -429,6 +682,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) ws
         s_off[g] = off;
         s_stg[g] = staged;
       }
+      }  // !bw
     }
     __syncthreads();
     if (b < p.nblk) {  // from here on thread t owns block tile * TB + t, as in the other walks
@@ -609,7 +863,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || TB <= 256 ? 256 : TB) ws
   __syncthreads();
   WSC_STAMP(2, __builtin_amdgcn_s_memrealtime());
   uint32_t en_b = 0;  // this thread's block's first entry (kWalkLaneView's view loop)
-  const uint32_t off_b = MODE != kWalkGroup ? lane_off : 0u;
+  const uint32_t off_b = !GW ? lane_off : 0u;
   if (b < p.nblk) {
     uint32_t on = s_ex[0], ok = s_ex[1], ov = s_ex[2];
     for (uint32_t w = 0; w < wave; w++) {
@@ -1315,7 +1569,11 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
 
 hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mid) {
   const uint32_t nblk = p.nblk;
-  if (p.wwalk == kWalkGroup && p.wlanes == 2)
+  if (p.wwalk == kWalkGroup && p.wlanes == 8 && p.wbidir == 2)  // 16 lanes forward + 16 backward
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroupBi, 8>), dim3((nblk + 7) / 8), dim3(256), 0, s, p);
+  else if (p.wwalk == kWalkGroup && p.wlanes == 8 && p.wbidir)  // 8 lanes forward + 8 backward
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroupBi, 16>), dim3((nblk + 15) / 16), dim3(256), 0, s, p);
+  else if (p.wwalk == kWalkGroup && p.wlanes == 2)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 128>), dim3((nblk + 127) / 128), dim3(256), 0, s, p);
   else if (p.wwalk == kWalkGroup && p.wlanes == 4)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 64>), dim3((nblk + 63) / 64), dim3(256), 0, s, p);
@@ -1352,10 +1610,12 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
   hipError_t e = hipGetLastError();
 #ifdef LSMGPU_STAMPS
   if (e == hipSuccess && p.stamps) {  // diagnostics: the walk's per-tile timeline
-    const uint32_t tb = p.wwalk == kWalkGroup ? 256 / p.wlanes
+    const uint32_t tb = p.wwalk == kWalkGroup ? (p.wbidir && p.wlanes == 8 ? 16 / p.wbidir : 256 / p.wlanes)
                       : (p.wwide ? p.wwide : (p.wfuse && p.wkeep && p.wtile == 192) || p.wtile == 192 ? 192 : 256);
     const uint32_t nt = (nblk + tb - 1) / tb;
     std::vector<uint64_t> h((size_t)nt * 4);
+    uint64_t cnt[4];
+    (void)hipMemcpyAsync(cnt, p.stamps + 8, sizeof(cnt), hipMemcpyDeviceToHost, s);
     (void)hipMemcpyAsync(h.data(), p.stamps + 16, h.size() * 8, hipMemcpyDeviceToHost, s);
     (void)hipStreamSynchronize(s);
     uint64_t t0 = ~0ull, t1 = 0;
@@ -1381,6 +1641,10 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
             "p90 %.2f max %.2f\n", nt, tb, (t1 - t0) / 100.0, walk / nt / 100.0, look / nt / 100.0,
             epi / nt / 100.0, pct(starts, 0.5), pct(starts, 0.9), starts.back(), pct(ends, 0.1),
             pct(ends, 0.5), pct(ends, 0.9), ends.back());
+    if (cnt[2])
+      fprintf(stderr, "[lsmgpu] group walk rounds per block: mean %.2f max %llu over %llu blocks, "
+              "chains met in %llu\n", (double)cnt[0] / cnt[2], (unsigned long long)cnt[1],
+              (unsigned long long)cnt[2], (unsigned long long)cnt[3]);
     if (const char* f = getenv("LSMGPU_STAMPS_FILE")) {
       if (FILE* o = fopen(f, "a")) {
         for (uint32_t t = 0; t < nt; t++)

@@ -57,6 +57,7 @@ struct DecodeParams {
   uint32_t wwide;           // lane walks: 0 (256-block tiles, 4 per CU) or 576 (2 per CU)
   uint32_t wlbfull;         // walk: every thread of a tile sums predecessor aggregates (no windows)
   uint32_t wpad;            // lane walk (256-block tiles): dynamic LDS bytes (residency experiments)
+  uint32_t wbidir;          // group walk: 8 lanes forward + 8 backward per block (kWalkGroupBi)
   uint32_t wscopy;          // 64-lane staged group walk: each wave copies its block from LDS
   uint32_t wslot;           // 64-lane staged group walk: 0 = kStageSlot, 1 = kStageSlotSmall
   uint32_t wsub;            // group walk: odd-shaped entries re-guessed inside a round
@@ -236,6 +237,7 @@ hipError_t launch_bloom_json(const BloomJson& p, hipStream_t s);
 // walk-scan-copy walk modes (DecodeParams::wwalk)
 constexpr int kWalkLane = 0;    // one lane per block, header by header from HBM
 constexpr int kWalkGroup = 2;   // wlanes lanes per block, speculative same-shape runs from HBM
+constexpr int kWalkGroupBi = 4; // the group walk plus a backward group per block (p.wbidir)
 // the 64-lane group walk's LDS slot per block (bytes): 4 slots + rows leave 2 workgroups per CU
 constexpr uint32_t kStageSlot = 19456;
 constexpr uint32_t kStageSlotSmall = 4352;  // (LSMGPU_WSC_SLOT=small: C2's <= 4.2 KiB blocks)

@@ -510,7 +510,8 @@ def test_wsc_lanes_per_entry(codec, oracle, monkeypatch, lanes):
 @pytest.mark.parametrize("walk", ["lane", "lane16", "lane192", "lane576", "lane_flush", "lane_viewsearch", "group", "group2",
                                   "group4", "group16", "group32", "group64", "group64_copy", "group64s",
                                   "group64g", "group64g_copy", "group_sub", "group16_sub",
-                                  "group_dpp", "lane_lbwin", "lane576_lbwin", "group_lbwin"])
+                                  "group_dpp", "lane_lbwin", "lane576_lbwin", "group_lbwin",
+                                  "group_bidir", "group_bidir_lbwin", "group_bidir16"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     """Walk-scan-copy's walks (LSMGPU_WSC_WALK): one lane per block from HBM, or 8 / 4
@@ -521,6 +522,7 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     tile and a block ending at the buffer's end (plus C5 32 KiB blocks for the HBM walks)."""
     from lsmdb_amd.codec import MODE_MATERIALIZE, MODE_VIEW
     monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
+    monkeypatch.setenv("LSMGPU_WSC_BIDIR", "0")  # (the group walk's default adds a backward group)
     if walk.endswith("_lbwin"):  # the windowed decoupled look-back (LSMGPU_WSC_LOOKBACK=window)
         monkeypatch.setenv("LSMGPU_WSC_LOOKBACK", "window")
         walk = walk[:-len("_lbwin")]
@@ -542,6 +544,9 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     elif walk == "group64s":  # the staged walk with 4.25 KiB slots (longer blocks from HBM)
         monkeypatch.setenv("LSMGPU_WSC_WALK", "group64")
         monkeypatch.setenv("LSMGPU_WSC_SLOT", "small")
+    elif walk.startswith("group_bidir"):  # 8 (16) lanes forward + 8 (16) backward per block
+        monkeypatch.setenv("LSMGPU_WSC_WALK", "group")
+        monkeypatch.setenv("LSMGPU_WSC_BIDIR", "2" if walk.endswith("16") else "1")
     elif walk == "group_dpp":  # the group's lane exchange by DPP OR-reductions
         monkeypatch.setenv("LSMGPU_WSC_WALK", "group")
         monkeypatch.setenv("LSMGPU_WSC_DPP", "1")
@@ -647,7 +652,7 @@ def _block_entries(block):
 
 
 @pytest.mark.parametrize("walk", ["lane", "lane16", "lane192", "lane576", "group", "group32", "group64",
-                                  "group64g", "group_sub"])
+                                  "group64g", "group_sub", "group_bidir", "group_bidir16"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
     """Blocks built to defeat a header-pattern filter, decoded by every walk.  Keys and
@@ -655,12 +660,15 @@ def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
     sometimes match.  Values are zero-filled, or carry planted fake chained headers: a
     candidate whose successor's prev points back at it is accepted, so verification must send
     the block to the serial walk.  Others carry fake terminators, or blocks are cut short (no
-    terminator, a torn terminator, torn entries).  Every block must decode exactly as the
-    oracle's iterator does."""
+    terminator, a torn terminator, torn entries), or carry false backward chains (a fake entry
+    inside a value that ends exactly at the next header, which names it as prev).  Every block
+    must decode exactly as the oracle's iterator does."""
     from lsmdb_amd.codec import MODE_MATERIALIZE, MODE_VIEW
     monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
     monkeypatch.setenv("LSMGPU_WSC_WALK", "lane" if walk in ("lane16", "lane192", "lane576")
-                       else walk.replace("_sub", ""))
+                       else walk.replace("_sub", "").replace("_bidir16", "").replace("_bidir", ""))
+    monkeypatch.setenv("LSMGPU_WSC_BIDIR", "2" if walk.endswith("_bidir16")
+                       else ("1" if walk.endswith("_bidir") else "0"))
     monkeypatch.setenv("LSMGPU_WSC_WIDE", "1" if walk == "lane576" else "0")
     monkeypatch.setenv("LSMGPU_WSC_SUB", "1" if walk.endswith("_sub") else "0")
     if walk == "group64g":
@@ -699,6 +707,17 @@ def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
             elif kind == 1 and vlen >= 13:  # a fake terminator inside a value
                 p = vstart + int(rng.integers(0, vlen - 12))
                 kd[o + p:o + p + 6] = bytes([0, 0, 0, 0, 0, 3])
+            elif kind == 3 and vlen >= 30 and rng.random() < 0.5:
+                # a false backward chain: a fake entry inside this value ending exactly where the
+                # next header (or the terminator) starts, which names it as its prev -- a walk
+                # from the terminator over prev fields accepts it; the iterator never sees it
+                end = vstart + vlen
+                p = vstart + int(rng.integers(0, vlen - 29))
+                fv = end - p - 11
+                kd[o + p:o + p + 10] = bytes([0, 0, 0, 1, fv >> 8, fv & 255]) + pos.to_bytes(4, "big")
+                if end + 10 <= n:
+                    kd[o + end + 6:o + end + 10] = p.to_bytes(4, "big")
+                planted += 1
         if kind == 2 and ents:  # cut: no terminator / torn terminator / torn last entry
             cut = [13, 1, 5, 20][(b // 4) % 4]
             lens[b] = max(0, n - cut)
