@@ -450,7 +450,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
   __shared__ uint32_t s_res[4][kRes];  // group / wave walk: n, K, V, status per block
   __shared__ uint32_t s_stg[kRes];  // group walk: the block is in its LDS slot (kStaged)
   __shared__ uint32_t s_cb[3][kWave64 ? TB : 1];  // p.wscopy: each block's output bases
-  __shared__ uint8_t s_mark[KEEP ? kWaves : 1][128];  // kWalkLaneView, p.wview: owner marks (lane + 1)
+  __shared__ uint8_t s_mark[KEEP || !GW ? kWaves : 1][128];  // kWalkLaneView, p.wview: owner marks (lane + 1)
   // the staged walk copying its own blocks (p.wscopy): no records for a copy launch
   const bool scopy = kWave64 && p.wscopy && !p.wfuse;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
@@ -477,6 +477,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
   const uint32_t b = tid < TB ? tile * TB + tid : 0xffffffffu;
   uint32_t n = 0, K = 0, V = 0, st = LSMGPU_BLK_OK;
   uint32_t lane_off = 0;  // lane walks: this thread's block offset
+  bool plen_b = false;    // lane walks: the block holds prefix-compressed entries
   if constexpr (GW) {
     // L lanes per block: each round the group reads the headers at pos + k * stride (stride =
     // the last accepted entry's size) and accepts the leading run whose guesses were right --
@@ -795,7 +796,8 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
       t[0] = n;
       t[1] = K;
       t[2] = V;
-      p.wstatus[b] = st | (K != pos - 10 * n - V ? kPlenFlag : 0u);  // see kPlenFlag
+      plen_b = K != pos - 10 * n - V;
+      p.wstatus[b] = st | (plen_b ? kPlenFlag : 0u);  // see kPlenFlag
     }
   }
   // tile scan (saturating u32: a key stream past 4 GiB - 1 fails the copy's capacity check)
@@ -863,6 +865,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
   __syncthreads();
   WSC_STAMP(2, __builtin_amdgcn_s_memrealtime());
   uint32_t en_b = 0;  // this thread's block's first entry (kWalkLaneView's view loop)
+  uint32_t ek_b = 0, ev_b = 0;  // and its key / value stream bases (p.weo)
   const uint32_t off_b = !GW ? lane_off : 0u;
   if (b < p.nblk) {
     uint32_t on = s_ex[0], ok = s_ex[1], ov = s_ex[2];
@@ -874,6 +877,8 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
     const uint32_t en = sat_add(on, in_ - n), ek = sat_add(ok, ik == 0xffffffffu ? ik : ik - K),
                    ev = sat_add(ov, iv - V);
     en_b = en;
+    ek_b = ek;
+    ev_b = ev;
     if (scopy) {
       s_cb[0][tid] = en;
       s_cb[1][tid] = ek;
@@ -932,6 +937,62 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
           else
             copy_block(p, bw, meta, pre, nw, Kw, Vw, sw, enw, ekw, evw, off, 0, 1, lane,
                        GlobalBytes{p.data + off});
+        }
+      }
+    }
+    if constexpr (!GW && !KEEP) {
+      // p.weo (lane walks, materialize): the per-entry outputs -- key_end, val_end and the view
+      // records -- written here, each wave its 64 blocks' entries (consecutive in the output),
+      // one lane per entry, from the records this wave flushed (L2-hot).  From the copy kernel
+      // (entry_outputs) the 68 MB cost 0.044 ms of C2's copy (profiles/r05r): its stores start
+      // at every block's first entry, into lines shared with blocks copied on other XCDs.
+      // Blocks with prefix-compressed entries keep them in the copy (copy_entries_plen).
+      if (p.weo && (p.mode & LSMGPU_MODE_MATERIALIZE)) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // this wave's record flushes
+        __builtin_amdgcn_wave_barrier();
+        const bool valid = b < p.nblk;
+        const uint32_t wb0 = tile * TB + wave * 64;
+        const uint32_t pw = in_ - n;  // wave-exclusive first entry of this lane's block
+        const uint32_t T = __builtin_amdgcn_readlane(in_, 63);  // the wave's entries
+        const uint64_t ew = __builtin_amdgcn_readlane(en_b, 0);  // the wave's first output entry
+        const bool view = (p.mode & LSMGPU_MODE_VIEW) && p.view;
+        auto emit = [&](uint32_t f, uint32_t L) {
+          const uint32_t pL = (uint32_t)__shfl((int)pw, (int)L), nL = (uint32_t)__shfl((int)n, (int)L);
+          const uint32_t ekL = (uint32_t)__shfl((int)ek_b, (int)L), evL = (uint32_t)__shfl((int)ev_b, (int)L);
+          const uint32_t offL = (uint32_t)__shfl((int)off_b, (int)L);
+          const uint32_t plL = (uint32_t)__shfl((int)(plen_b ? 1u : 0u), (int)L);
+          if (f >= T || plL) return;
+          const uint64_t bend = ew + pL + nL;
+          if (!(bend <= p.ent_cap && bend <= 0xffffffffull)) return;  // reported (result[5])
+          const uint32_t e = f - pL;
+          const uint32_t* meta = p.wmeta + (uint64_t)(wb0 + L) * p.wcap;
+          const uint32_t m0 = meta[e], m1 = meta[e + 1];
+          const uint32_t hp1 = m1 & 0xffffu, vo1 = m1 >> 16;
+          if (p.key_end) p.key_end[ew + f] = ekL + hp1 - 10 * (e + 1) - vo1;
+          if (p.val_end) p.val_end[ew + f] = evL + vo1;
+          if (view) {
+            const uint32_t hp = m0 & 0xffffu, vl = vo1 - (m0 >> 16), kl = hp1 - hp - 10 - vl;
+            p.view[ew + f] = (uint64_t)(offL + hp + 10) | ((uint64_t)kl << 32) | ((uint64_t)vl << 48);
+          }
+        };
+        // owners by one scatter and a max-scan (as the view epilogue below), 128 entries a trip
+        uint8_t* const mk = s_mark[wave];
+        mk[lane] = 0;
+        mk[64 + lane] = 0;
+        wave_lds_fence();
+        uint32_t carry = 0;
+        for (uint32_t c0 = 0; c0 < T; c0 += 128) {
+          if (valid && n > 0 && pw >= c0 && pw < c0 + 128) mk[pw - c0] = lane + 1;
+          wave_lds_fence();
+          const uint32_t a0 = mk[lane], a1 = mk[64 + lane];
+          mk[lane] = 0;
+          mk[64 + lane] = 0;
+          const uint32_t v0 = max(wave_scan_max(a0, lane), carry);
+          const uint32_t v1 = max(wave_scan_max(a1, lane), __builtin_amdgcn_readlane(v0, 63));
+          carry = __builtin_amdgcn_readlane(v1, 63);
+          wave_lds_fence();
+          emit(c0 + lane, v0 - 1);
+          emit(c0 + 64 + lane, v1 - 1);
         }
       }
     }
@@ -1522,21 +1583,23 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
   // raised the VGPRs from 44 to 90, 8 -> 5 waves per SIMD: removed)
   if (p.walign == 2 && mat && split == 1 && n < kWave && tab && chunks_fit(kbase, vbase, K, V)) {
     // dense aligned chunks over both streams (copy_chunks)
-    entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
+    if (!p.weo) entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
     const uint64_t lim = p.data_len - off;
     copy_chunks(blk, lim < 0xffffffffull ? (uint32_t)lim : 0xffffffffu, kbase, vbase, n, K, V, lane, pre, tab);
   } else if (p.walign == 1 && mat && split == 1) {
     // aligned output chunks + the stream edges byte by byte (copy_entries_aligned)
-    entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
+    if (!p.weo) entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
     if (p.wj == 16 || (p.wj == 0 && avg > 128))
       copy_entries_aligned<16, 2>(meta, blk, kbase, vbase, n, K, V, sub, split, lane, pre);
     else
       copy_entries_aligned<8, 5>(meta, blk, kbase, vbase, n, K, V, sub, split, lane, pre);
+  } else if ((p.wj == 16 || (p.wj == 0 && avg > 128)) && p.weo) {  // (outputs: the walk wrote them)
+    copy_entries<16, 2, false>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
   } else if (p.wj == 16 || (p.wj == 0 && avg > 128)) {
     copy_entries<16, 2, true>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
   } else {
     // (timing-only ablations: 8 no per-entry outputs, 16 no pieces)
-    if (!(p.ablate & 8)) entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
+    if (!(p.ablate & 8) && !p.weo) entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
     if (mat && !(p.ablate & 16))
       copy_entries<8, 5, false>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
   }

@@ -601,16 +601,18 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     _assert_same(codec.decode_host(tight, so, sl_), oracle.decode(tight, so, sl_), "tight end")
 
 
-@pytest.mark.parametrize("align", ["0", "1", "2"])
+@pytest.mark.parametrize("align", ["0", "1", "2", "0-eo1"])
 def test_wsc_mixed_copy(codec, oracle, monkeypatch, align):
     """Walk-scan-copy's copy over every entry shape in one batch: C2 / C3 blocks, random key
     and value lengths with zero-length values, > 128 entries per block, prefix-compressed KAT
     blocks, 32 KiB C5 blocks, blocks at odd offsets, and the last block ending at the buffer's
     end.  align (LSMGPU_WSC_ALIGN): 0 the unaligned 16-B pieces (default), 1 aligned chunks per
     entry group, 2 dense aligned chunks over both streams (copy_chunks: owner table, merges
-    across entries, partial head / tail chunks)."""
+    across entries, partial head / tail chunks); -eo1: the per-entry outputs from the lane
+    walk's epilogue instead of the copy kernel (LSMGPU_WSC_EO=1)."""
     monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
-    monkeypatch.setenv("LSMGPU_WSC_ALIGN", align)
+    monkeypatch.setenv("LSMGPU_WSC_ALIGN", align.split("-")[0])
+    monkeypatch.setenv("LSMGPU_WSC_EO", "1" if align.endswith("eo1") else "0")
     c2 = _cols(2, 30000, seed=31)
     c3 = _cols(3, 2000, seed=32)
     c5 = _cols(5, 3000, seed=33)
