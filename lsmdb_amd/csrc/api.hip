@@ -513,6 +513,8 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     // outputs instead of the copy (p.weo).  Off: same box, C2 copy 0.4992-0.5 -> 0.4547-0.4561 ms
     // but walk 0.2088-0.209 -> 0.2556-0.2569 ms (the epilogue's record re-reads are a dependent
     // chain per wave at 1 workgroup per CU), decode 1,402-1,404 -> 1,396-1,398 GiB/s (r05ac)
+    const char* es_env = getenv("LSMGPU_WSC_EOSEP");
+    p.weosep = es_env && atoi(es_env) == 1 ? 1u : 0u;
     const char* eo_env = getenv("LSMGPU_WSC_EO");
     p.weo = p.wwalk == kWalkLane && !p.wfuse && eo_env && atoi(eo_env) == 1 ? 1u : 0u;
     // the 64-lane staged walk copies its own blocks from LDS (no copy launch, one read of the

@@ -416,7 +416,11 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
   static_assert(kThreads % 64 == 0, "whole waves");
   // LDS row per lane: CH records (+ 1 pad, bank spread), or kViewRec kept records (+ 1; WIDE:
   // none, the 33-word stride is odd already)
-  constexpr uint32_t kStage = KEEP ? (WIDE ? kViewRec : kViewRec + 1) : CH + 1;
+  // kept records per block: 41 for the 576-block tiles (one workgroup per CU whatever their LDS;
+  // C2: 23 % of blocks have 33-37 entries and spilled to p.wmeta with 33), 33 for 256-block tiles
+  // (4 per CU)
+  constexpr uint32_t kRec = WIDE ? 41u : kViewRec;
+  constexpr uint32_t kStage = KEEP ? (WIDE ? kRec : kRec + 1) : CH + 1;
   constexpr uint32_t kStageBytes = kThreads * kStage * sizeof(uint32_t);
   // group walk: a 32-record ring per block (the walk's LDS also serves the view epilogue's
   // owner map)
@@ -738,7 +742,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
           const uint32_t end = pos + 10 + klen + vlen;             // iterator.go:101-109
           if (end > len) { st = LSMGPU_BLK_VALUE_OVERFLOW; done = true; break; }
           if constexpr (KEEP) {
-            if (n < kViewRec) row[n] = pos | (V << 16);
+            if (n < kRec) row[n] = pos | (V << 16);
             else p.wmeta[(uint64_t)b * p.wcap + n] = pos | (V << 16);
           } else {
             row[n & (CH - 1)] = pos | (V << 16);
@@ -773,7 +777,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
     // sentinel are never read)
     if constexpr (KEEP) {  // the sentinel; the rows stay in LDS
       if (valid) {
-        if (n < kViewRec) row[n] = pos | (V << 16);
+        if (n < kRec) row[n] = pos | (V << 16);
         else p.wmeta[(uint64_t)b * p.wcap + n] = pos | (V << 16);
       }
     }
@@ -1020,8 +1024,8 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
       const uint32_t e = f - pL;
       const uint32_t* rw = stage + (wave * 64 + L) * kStage;
       const uint32_t* gl = p.wmeta + (uint64_t)(wb0 + L) * p.wcap;
-      const uint32_t m0 = e < kViewRec ? rw[e] : gl[e];
-      const uint32_t m1 = e + 1 < kViewRec ? rw[e + 1] : gl[e + 1];
+      const uint32_t m0 = e < kRec ? rw[e] : gl[e];
+      const uint32_t m1 = e + 1 < kRec ? rw[e + 1] : gl[e + 1];
       const uint32_t hp = m0 & 0xffffu, vl = (m1 >> 16) - (m0 >> 16);
       const uint32_t kl = (m1 & 0xffffu) - hp - 10 - vl;  // stored key bytes
       p.view[ew + f] = (uint64_t)(offL + hp + 10) | ((uint64_t)kl << 32) | ((uint64_t)vl << 48);
@@ -1593,7 +1597,12 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
       copy_entries_aligned<16, 2>(meta, blk, kbase, vbase, n, K, V, sub, split, lane, pre);
     else
       copy_entries_aligned<8, 5>(meta, blk, kbase, vbase, n, K, V, sub, split, lane, pre);
-  } else if ((p.wj == 16 || (p.wj == 0 && avg > 128)) && p.weo) {  // (outputs: the walk wrote them)
+  } else if ((p.wj == 16 || (p.wj == 0 && avg > 128)) && (p.weo || p.weosep || !mat)) {
+    // (outputs: the walk wrote them, or one lane per entry first: a view-only decode through
+    // the copy kernel (C5 view 0.270 -> 0.238 ms, profiles/r05ae), or LSMGPU_WSC_EOSEP=1 -- for
+    // materialize the 16-lane groups' own writes stay faster: C5 copy 0.607 vs 0.617 ms, C3
+    // 0.494-0.498 vs 0.508-0.510)
+    if (!p.weo && !(p.ablate & 8)) entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
     copy_entries<16, 2, false>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
   } else if (p.wj == 16 || (p.wj == 0 && avg > 128)) {
     copy_entries<16, 2, true>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);

@@ -185,7 +185,23 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
       const uint32_t edge = i == 0 ? carry : readlane(pos[i - 1], kWave - J);
       const uint64_t r = e0 + i * EPP + lane / J;
       const uint32_t prev = r == 0 ? 0xffffffffu : (lane < J ? edge : below) - bs;  // builder.go:95-99
-      if (on[i] && j == 0) store_header(out + pos[i], klen[i], vlen[i], prev);
+      if (on[i] && j == 0) {
+        if (p.hdr16 && klen[i] >= 8) {  // (8-B key read inside the key)
+          // the header and the key's first 6 bytes as one 16-B store (the key's first piece
+          // rewrites those 6 bytes with the same values): one store instruction per pass instead
+          // of an 8-B and a 2-B one
+          uint2 k8;
+          __builtin_memcpy(&k8, p.keys + sk[i], 8);
+          uint4 w;
+          w.x = bswap16(klen[i]) << 16;                               // plen 00 00 | klen BE
+          w.y = bswap16(vlen[i]) | (bswap16(prev >> 16) << 16);       // vlen BE | prev[31:16] BE
+          w.z = bswap16(prev & 0xffffu) | (k8.x << 16);               // prev[15:0] BE | key[0..1]
+          w.w = (k8.x >> 16) | (k8.y << 16);                          // key[2..5]
+          __builtin_memcpy(out + pos[i], &w, 16);
+        } else {
+          store_header(out + pos[i], klen[i], vlen[i], prev);
+        }
+      }
       if (on[i] && j == 1 && r == m - 1) {  // terminator + restart (builder.go:121-123,146-160)
         const uint32_t te = pos[i] + 10 + klen[i] + vlen[i];
         uint8_t* t = out + te;
@@ -302,8 +318,13 @@ static hipError_t launch_enc(const EncodeParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_encode(const EncodeParams& p, int num_cus, hipStream_t s) {
+hipError_t launch_encode(const EncodeParams& p0, int num_cus, hipStream_t s) {
   (void)num_cus;
+  EncodeParams p = p0;
+  // one 16-B store for the header and the key's first 6 bytes (same box, C2 encode 0.5864-0.5895
+  // -> 0.5627-0.5667 ms, profiles/r05ae); LSMGPU_ENC_HDR16=0: the 8-B + 2-B header stores
+  const char* h16 = getenv("LSMGPU_ENC_HDR16");
+  p.hdr16 = h16 && atoi(h16) == 0 ? 0u : 1u;
   // J = lanes per entry ~ the average entry's 16-B pieces (C2: 129 B -> 8; C3: ~1.1 KB -> 64)
   const uint64_t avg = p.n ? (p.key_total + p.vs_total) / p.n : 120;
   const char* ge = getenv("LSMGPU_ENC_G");  // A/B: entry-group passes per loop trip

@@ -59,6 +59,7 @@ struct DecodeParams {
   uint32_t wpad;            // lane walk (256-block tiles): dynamic LDS bytes (residency experiments)
   uint32_t wbidir;          // group walk: 8 lanes forward + 8 backward per block (kWalkGroupBi)
   uint32_t weo;             // lane walk (materialize): the walk writes key_end / val_end / view
+  uint32_t weosep;          // copy, 16 lanes per entry: per-entry outputs in a separate pass
   uint32_t wscopy;          // 64-lane staged group walk: each wave copies its block from LDS
   uint32_t wslot;           // 64-lane staged group walk: 0 = kStageSlot, 1 = kStageSlotSmall
   uint32_t wsub;            // group walk: odd-shaped entries re-guessed inside a round
@@ -93,6 +94,7 @@ struct EncodeParams {
   const uint32_t* src;
   const uint32_t* src_key_end;
   const uint32_t* src_vs_end;
+  uint32_t hdr16;  // set by launch_encode: header + the key's first 6 bytes as one 16-B store
 };
 
 // Builder.ReachedCapacity table cut over a sorted entry stream (encode.hip)

@@ -474,7 +474,8 @@ def test_wsc_many_tiles(codec, oracle, monkeypatch, chunk, lookback):
 
 @pytest.mark.parametrize("knob,val", [("LSMGPU_ENC_J", "4"), ("LSMGPU_ENC_J", "8"),
                                       ("LSMGPU_ENC_J", "16"), ("LSMGPU_ENC_G", "2"),
-                                      ("LSMGPU_ENC_G", "4")])
+                                      ("LSMGPU_ENC_G", "4"), ("LSMGPU_ENC_HDR16", "1"),
+                                      ("LSMGPU_ENC_HDR16", "0")])
 def test_encode_template_instances(codec, oracle, monkeypatch, knob, val):
     """Every encode_kernel<J, G> instance the A/B knobs select (LSMGPU_ENC_J / LSMGPU_ENC_G)
     changes which passes take the lane-shuffle offset path (advisor, round 1): each is checked
