@@ -490,6 +490,13 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     const uint64_t cus = (uint64_t)c->num_cus;
     p.wwide = ww_env ? (atoi(ww_env) != 0 ? 576u : 0u)
                      : ((nblk + 255) / 256 > 4 * cus && (nblk + 575) / 576 <= 2 * cus ? 576u : 0u);
+    // wide tiles: just enough blocks for two equal waves of tiles at one workgroup per CU (C2
+    // 2^30 B: 521 blocks, 512 tiles; same box, walk 0.2099-0.2108 -> 0.2062-0.2089 ms, view
+    // 0.2314 -> 0.228-0.2283 ms, profiles/r05af), or LSMGPU_WSC_TBE=0: 576 blocks each
+    const char* tbe_env = getenv("LSMGPU_WSC_TBE");
+    p.wtbe = 576u;
+    if (p.wwide && !(tbe_env && atoi(tbe_env) == 0))
+      p.wtbe = (uint32_t)std::min<uint64_t>(576, std::max<uint64_t>(64, (nblk + 2 * cus - 1) / (2 * cus)));
 
     const char* wk_env = getenv("LSMGPU_WSC_WALK");
     // Default: 8 lanes per block guessing same-shape runs (kWalkGroup) when the batch has at

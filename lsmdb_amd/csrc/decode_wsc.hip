@@ -458,7 +458,10 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
   // the staged walk copying its own blocks (p.wscopy): no records for a copy launch
   const bool scopy = kWave64 && p.wscopy && !p.wfuse;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-  const uint32_t ntiles = (p.nblk + TB - 1) / TB;
+  // blocks per tile: TB, or for the wide lane walks p.wtbe <= TB (threads past it hold no block):
+  // tiles sized so the two waves of tiles (one workgroup per CU) carry equal shares
+  const uint32_t TBe = WIDE && p.wtbe ? p.wtbe : TB;
+  const uint32_t ntiles = (p.nblk + TBe - 1) / TBe;
 #ifdef LSMGPU_STAMPS
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -477,8 +480,8 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
   // (the look-back timeout, result[5] |= 2) can be set before this and then erased
   if (p.zero_result && tile == 0 && tid < 8)
     atomicExch(reinterpret_cast<unsigned long long*>(p.result + tid), 0ull);
-  // thread t owns block tile * TB + t (threads past TB own none: zero entries)
-  const uint32_t b = tid < TB ? tile * TB + tid : 0xffffffffu;
+  // thread t owns block tile * TBe + t (threads past TBe own none: zero entries)
+  const uint32_t b = tid < TBe ? tile * TBe + tid : 0xffffffffu;
   uint32_t n = 0, K = 0, V = 0, st = LSMGPU_BLK_OK;
   uint32_t lane_off = 0;  // lane walks: this thread's block offset
   bool plen_b = false;    // lane walks: the block holds prefix-compressed entries
@@ -726,7 +729,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
       done = true;
     }
     const uint8_t* blk = p.data + off;
-    const uint32_t wb0 = tile * TB + wave * 64;  // the block of this wave's lane 0
+    const uint32_t wb0 = tile * TBe + wave * 64;  // the block of this wave's lane 0
     for (uint32_t k = 0;; k++) {
       if (__ballot(!done) == 0) break;
       bool rec = false;
@@ -955,7 +958,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // this wave's record flushes
         __builtin_amdgcn_wave_barrier();
         const bool valid = b < p.nblk;
-        const uint32_t wb0 = tile * TB + wave * 64;
+        const uint32_t wb0 = tile * TBe + wave * 64;
         const uint32_t pw = in_ - n;  // wave-exclusive first entry of this lane's block
         const uint32_t T = __builtin_amdgcn_readlane(in_, 63);  // the wave's entries
         const uint64_t ew = __builtin_amdgcn_readlane(en_b, 0);  // the wave's first output entry
@@ -1009,7 +1012,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
     // entry, 64 consecutive 8-B records per store instruction, from the rows its lanes filled
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // rows (and any spill) written
     __builtin_amdgcn_wave_barrier();
-    const uint32_t wb0 = tile * TB + wave * 64;
+    const uint32_t wb0 = tile * TBe + wave * 64;
     const uint32_t pw = in_ - n;  // wave-exclusive first entry of this lane's block
     const uint32_t T = __builtin_amdgcn_readlane(in_, 63);  // the wave's entries (no saturation:
                                                            // <= 64 x 6,554)
@@ -1662,9 +1665,9 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
   else if (p.wwalk == kWalkGroup)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 32>), dim3((nblk + 31) / 32), dim3(256), 0, s, p);
   else if (p.wfuse && p.wkeep && p.wwide == 576)
-    hipLaunchKernelGGL((wsc_walk_kernel<kWalkLaneView, 576>), dim3((nblk + 575) / 576), dim3(576), 0, s, p);
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkLaneView, 576>), dim3((nblk + p.wtbe - 1) / p.wtbe), dim3(576), 0, s, p);
   else if (!p.wfuse && p.wwide == 576 && p.wchunk == 32)
-    hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 576>), dim3((nblk + 575) / 576), dim3(576), 0, s, p);
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 576>), dim3((nblk + p.wtbe - 1) / p.wtbe), dim3(576), 0, s, p);
   else if (p.wfuse && p.wkeep && p.wtile == 192)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLaneView, 192>), dim3((nblk + 191) / 192), dim3(192), 0, s, p);
   else if (p.wfuse && p.wkeep)
@@ -1683,7 +1686,7 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
 #ifdef LSMGPU_STAMPS
   if (e == hipSuccess && p.stamps) {  // diagnostics: the walk's per-tile timeline
     const uint32_t tb = p.wwalk == kWalkGroup ? (p.wbidir && p.wlanes == 8 ? 16 / p.wbidir : 256 / p.wlanes)
-                      : (p.wwide ? p.wwide : (p.wfuse && p.wkeep && p.wtile == 192) || p.wtile == 192 ? 192 : 256);
+                      : (p.wwide ? p.wtbe : (p.wfuse && p.wkeep && p.wtile == 192) || p.wtile == 192 ? 192 : 256);
     const uint32_t nt = (nblk + tb - 1) / tb;
     std::vector<uint64_t> h((size_t)nt * 4);
     uint64_t cnt[4];

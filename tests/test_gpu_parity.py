@@ -512,7 +512,7 @@ def test_wsc_lanes_per_entry(codec, oracle, monkeypatch, lanes):
                                   "group4", "group16", "group32", "group64", "group64_copy", "group64s",
                                   "group64g", "group64g_copy", "group_sub", "group16_sub",
                                   "group_dpp", "lane_lbwin", "lane576_lbwin", "group_lbwin",
-                                  "group_bidir", "group_bidir_lbwin", "group_bidir16"])
+                                  "group_bidir", "group_bidir_lbwin", "group_bidir16", "lane576tbe"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     """Walk-scan-copy's walks (LSMGPU_WSC_WALK): one lane per block from HBM, or 8 / 4
@@ -533,9 +533,11 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     elif walk == "lane192":  # lane-walk workgroups of 192 blocks
         monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
         monkeypatch.setenv("LSMGPU_WSC_TILE", "192")
-    elif walk == "lane576":  # wide lane-walk tiles (576 blocks, 9 waves: the 2^30-B default)
+    elif walk.startswith("lane576"):  # wide lane-walk tiles (576 blocks, 9 waves: the 2^30-B default)
         monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
         monkeypatch.setenv("LSMGPU_WSC_WIDE", "1")
+        # tbe: tiles of fewer blocks than threads (two equal waves; here 64 blocks per tile)
+        monkeypatch.setenv("LSMGPU_WSC_TBE", "1" if walk.endswith("tbe") else "0")
     elif walk == "lane_viewsearch":  # view-only: owners by lane-shuffle binary search
         monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
         monkeypatch.setenv("LSMGPU_WSC_VIEWSCAN", "0")
