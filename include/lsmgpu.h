@@ -84,6 +84,9 @@ int lsmgpu_kernel_times(lsmgpu_ctx* ctx, float* walk_ms, float* copy_ms);
 int lsmgpu_stream_probe_async(lsmgpu_ctx* ctx, int kind, const void* d_src, void* d_dst,
                               uint64_t bytes, uint32_t wg_per_cu);
 const char* lsmgpu_strerror(int code);
+/* The HIP call behind this thread's last LSMGPU_ERR_HIP ("call -> HIP error string (where)"),
+ * "" if none yet.  Valid until this thread's next failing call. */
+const char* lsmgpu_last_error(void);
 int lsmgpu_abi_version(void);
 
 /* Replaces Table.readIndex's tail parse (table/table.go:177-215): bloom length + bloom span,

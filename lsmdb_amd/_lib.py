@@ -49,6 +49,7 @@ EXPORTED_SYMBOLS = (
     "lsmgpu_set_kernel_timing",
     "lsmgpu_kernel_times",
     "lsmgpu_strerror",
+    "lsmgpu_last_error",
     "lsmgpu_abi_version",
     "lsmgpu_parse_index",
     "lsmgpu_open_tables_async",
@@ -136,6 +137,8 @@ class LsmgpuError(RuntimeError):
     def __init__(self, code: int, what: str = ""):
         self.code = code
         msg = _LIB.lsmgpu_strerror(code).decode() if _LIB is not None else str(code)
+        if code == ERR_HIP and _LIB is not None and hasattr(_LIB, "lsmgpu_last_error"):
+            msg += f" [{_LIB.lsmgpu_last_error().decode()}]"  # the failing HIP call
         super().__init__(f"{what}: {msg} (code {code})" if what else f"{msg} (code {code})")
 
 
@@ -173,6 +176,9 @@ def _load() -> ctypes.CDLL:
     lib.lsmgpu_kernel_times.restype = c_int
     lib.lsmgpu_strerror.argtypes = [c_int]
     lib.lsmgpu_strerror.restype = ctypes.c_char_p
+    if hasattr(lib, "lsmgpu_last_error"):
+        lib.lsmgpu_last_error.argtypes = []
+        lib.lsmgpu_last_error.restype = ctypes.c_char_p
     lib.lsmgpu_abi_version.argtypes = []
     lib.lsmgpu_abi_version.restype = c_int
     lib.lsmgpu_parse_index.argtypes = [c_void_p, c_uint64, c_void_p, c_void_p, c_uint64,

@@ -87,6 +87,9 @@ hipError_t bounce_copy(void* dst, const void* src, uint64_t n, hipMemcpyKind kin
 // a copy from the registration its first byte lies in and rejects one that runs past that
 // registration's end (a buffer whose edge pages another caller pinned, or a neighbour's).  Every
 // host copy of the library goes through here; a piece HIP refuses goes through bounce_copy.
+// hcopy's account of a failed piece (its range, HIP's view of the host pointer), joined to the
+// next reported HIP error (lsmgpu_last_error)
+static thread_local char t_hcopy_detail[160] = "";
 hipError_t hcopy(void* dst, const void* src, uint64_t n, hipMemcpyKind kind, hipStream_t s) {
   if (!n) return hipSuccess;
   const bool h2d = kind == hipMemcpyHostToDevice;
@@ -101,7 +104,10 @@ hipError_t hcopy(void* dst, const void* src, uint64_t n, hipMemcpyKind kind, hip
     void* d = static_cast<uint8_t*>(dst) + o;
     const void* q = static_cast<const uint8_t*>(src) + o;
     hipError_t e = hipMemcpyAsync(d, q, m, kind, s);
-    if (e == hipErrorInvalidValue) {
+    // (any refusal, not only hipErrorInvalidValue: a sporadic host-path ERR_HIP in round 5's
+    // suite (encode_blocks from numpy memory after register / unregister cycles at re-used
+    // addresses) named no call; the bounce does not depend on what the runtime believes)
+    if (e != hipSuccess) {
       static const bool dbg = getenv("LSMGPU_DEBUG_ERR") != nullptr;
       if (dbg)
         fprintf(stderr, "lsmgpu: hcopy %s host piece [%#lx, %#lx) of [%#lx, %#lx) refused (%s): bounce\n",
@@ -110,7 +116,16 @@ hipError_t hcopy(void* dst, const void* src, uint64_t n, hipMemcpyKind kind, hip
       (void)hipGetLastError();
       e = bounce_copy(d, q, m, kind, s);
     }
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess) {
+      hipPointerAttribute_t a{};
+      const hipError_t ea = hipPointerGetAttributes(&a, reinterpret_cast<const void*>(r.first));
+      snprintf(t_hcopy_detail, sizeof(t_hcopy_detail), "%s piece [%#lx, %#lx) of [%#lx, %#lx), %zu pieces, "
+               "host pointer type %d (query %d)", h2d ? "H2D" : "D2H", (unsigned long)r.first,
+               (unsigned long)r.second, (unsigned long)h, (unsigned long)(h + n), pc.size(),
+               ea == hipSuccess ? (int)a.type : -1, (int)ea);
+      (void)hipGetLastError();
+      return e;
+    }
   }
   return hipSuccess;
 }
@@ -184,10 +199,15 @@ struct lsmgpu_ctx {
   uint64_t* h_chunk_res = nullptr;  // pinned, 8 u64 per slot
 };
 
-// LSMGPU_DEBUG_ERR=1: the failing HIP call and its error on stderr (diagnostics)
+// The failing HIP call and its error, kept per thread for lsmgpu_last_error; LSMGPU_DEBUG_ERR=1
+// also prints it on stderr
+static thread_local char t_last_error[256] = "";
 static void report_hip_error(const char* what, hipError_t e, int line) {
+  snprintf(t_last_error, sizeof(t_last_error), "%s -> %s (api.hip:%d)%s%s", what, hipGetErrorString(e), line,
+           t_hcopy_detail[0] ? ": " : "", t_hcopy_detail);
+  t_hcopy_detail[0] = 0;
   static const bool on = getenv("LSMGPU_DEBUG_ERR") != nullptr;
-  if (on) fprintf(stderr, "lsmgpu: %s -> %s (api.hip:%d)\n", what, hipGetErrorString(e), line);
+  if (on) fprintf(stderr, "lsmgpu: %s\n", t_last_error);
 }
 #define HIPC(x)                                    \
   do {                                             \
@@ -201,6 +221,8 @@ static void report_hip_error(const char* what, hipError_t e, int line) {
 extern "C" {
 
 int lsmgpu_abi_version(void) { return LSMGPU_ABI_VERSION; }
+
+const char* lsmgpu_last_error(void) { return t_last_error; }
 
 const char* lsmgpu_strerror(int code) {
   switch (code) {
