@@ -1618,6 +1618,10 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
 }
 
 // K2: one wave per block (p.wsplit waves above 8 KiB).
+// (Measured against it: two blocks per wave with the second block's words loaded during the first
+// block's pieces.  C2 copy 0.492 -> 0.598 ms at 64 VGPRs with 21 spilled, and -> 0.706 ms at 99
+// VGPRs, occupancy 4: the copy needs waves in flight more than it needs fewer metadata round
+// trips.  Profiles r05aj, r05ak.)
 __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   const uint32_t lane = lane_id();
   // p.wsplit waves share a block (large blocks): wave `sub` takes passes sub, sub + wsplit, ...

@@ -32,8 +32,9 @@ __global__ void probe(unsigned* ctr, unsigned* seen) {
 // the lane walk's shape: 576 threads, 76,268 B of STATIC LDS, launch bounds 576
 __global__ void __launch_bounds__(576) probe_static(unsigned* ctr, unsigned* seen) {
   __shared__ unsigned char big[76268];
+  for (unsigned i = threadIdx.x; i < 76268; i += blockDim.x) big[i] = (unsigned char)i;
+  __syncthreads();
   if (threadIdx.x == 0) {
-    big[threadIdx.x * 7 % 76268] = 1;
     unsigned v = atomicAdd(ctr, 1u) + 1;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     unsigned best = v;
@@ -42,7 +43,7 @@ __global__ void __launch_bounds__(576) probe_static(unsigned* ctr, unsigned* see
       best = v > best ? v : best;
       __builtin_amdgcn_s_sleep(4);
     }
-    atomicMax(seen, best + (big[5] & 0));
+    atomicMax(seen, best + (big[(v * 131u) % 76268u] == 255u ? 1u : 0u) * 0u + (big[77] != 77u));
     atomicSub(ctr, 1u);
   }
 }
