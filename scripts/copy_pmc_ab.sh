@@ -1,15 +1,17 @@
 #!/bin/bash
-# Copy kernel counters, aligned chunks (LSMGPU_WSC_ALIGN=1) vs unaligned pieces (0): SQ issue /
-# wait counters and L1 -> L2 request counts and latencies, one --pmc pass each.
-# Usage (on the GPU box): bash scripts/copy_pmc_ab.sh <tag> [config]
+# Copy kernel counters across LSMGPU_WSC_ALIGN modes (0 unaligned pieces, 1 aligned chunks per
+# entry group, 2 dense chunks, 3 chunks gathered from the block staged in LDS): SQ issue / wait,
+# LDS and occupancy counters, L1 -> L2 request counts and latencies, one --pmc pass each.
+# Usage (on the GPU box): MODES="3 0" bash scripts/copy_pmc_ab.sh <tag> [config]
 set -o pipefail
 T=${1:-copypmc}; C=${2:-2}
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/$T
 mkdir -p $O
 P="python3 bench.py --no-cpu --no-view --no-peaks --config $C --steps 3 --warmup 1"
-for A in 1 0; do
+for A in ${MODES:-1 0}; do
   for pass in "sq SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SALU" \
+              "lds SQ_LDS_BANK_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_WAIT_INST_LDS SQ_LEVEL_WAVES SQ_BUSY_CYCLES SQ_WAVES" \
               "tcp TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_WRITE_REQ_sum TCP_TCC_WRITE_REQ_LATENCY_sum" \
               "ea TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum"; do
     set -- $pass
