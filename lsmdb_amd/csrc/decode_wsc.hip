@@ -757,7 +757,9 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
           rec = true;
         } while (false);
       }
-      if (!KEEP && (k & (CH - 1)) == CH - 1) {
+      // (timing-only ablation 128: no record flush; honoured only with ablation 2, under which
+      // the copy reads no record -- a copy of stale records writes out of bounds)
+      if (!KEEP && (k & (CH - 1)) == CH - 1 && (p.ablate & 130) != 130) {
         const uint64_t fl = __ballot(rec);  // lanes holding records k-CH+1 .. k
         if (fl) {
           wave_lds_fence();
@@ -785,7 +787,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
       }
     }
     if (valid && !KEEP) row[n & (CH - 1)] = pos | (V << 16);
-    const uint64_t vm = KEEP ? 0ull : __ballot(valid);
+    const uint64_t vm = KEEP || (p.ablate & 258) == 258 ? 0ull : __ballot(valid);  // (ablation 256: as 128)
     if (!KEEP) wave_lds_fence();
     constexpr uint32_t kPer = CH / 4;
 #pragma unroll

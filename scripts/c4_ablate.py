@@ -1,5 +1,5 @@
 """Walk / copy kernel times under timing-only ablations (LSMGPU_ABLATE: 1 no look-back,
-2 no copy / no view records, 4 no walk) and walk knobs -- outputs are NOT checked (ablations
+2 no copy / no view records, 4 no walk, 128 / 256 no record flush, with 2 only) and walk knobs -- outputs are NOT checked (ablations
 break them).  C4 by default; --config 2 for C2 at 2^30 B.
     python scripts/c4_ablate.py [--config N]   (one process per setting, one line each)"""
 import json
@@ -14,7 +14,9 @@ SETTINGS = [("full", {}), ("no_lookback", {"LSMGPU_ABLATE": "1"}), ("no_walk", {
             ("lane", {"LSMGPU_WSC_WALK": "lane"})]
 SETTINGS_C2 = [("full", {}), ("no_lookback", {"LSMGPU_ABLATE": "1"}), ("no_walk", {"LSMGPU_ABLATE": "4"}),
                ("no_out", {"LSMGPU_ABLATE": "2"}), ("no_walk_no_out", {"LSMGPU_ABLATE": "6"}),
-               ("no_walk_lb_out", {"LSMGPU_ABLATE": "7"})]
+               ("no_walk_lb_out", {"LSMGPU_ABLATE": "7"}),
+               # record flushes (128: in the walk loop, 256: the last chunk) -- only with 2
+               ("no_out_no_flush", {"LSMGPU_ABLATE": "130"}), ("no_out_no_flush_all", {"LSMGPU_ABLATE": "386"})]
 
 
 def one(cfg):
