@@ -519,6 +519,12 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     p.wtbe = 576u;
     if (p.wwide && !(tbe_env && atoi(tbe_env) == 0))
       p.wtbe = (uint32_t)std::min<uint64_t>(576, std::max<uint64_t>(64, (nblk + 2 * cus - 1) / (2 * cus)));
+    // wide materialize walks: two tiles per workgroup, walked back to back before their
+    // look-backs (wsc_walk_persist_kernel; same box, C2 2^30 B: walk 0.2059-0.2066 ->
+    // 0.2011-0.2013 ms, decode 1,422 -> 1,435-1,436 GiB/s, profiles/r05ar); LSMGPU_WSC_PERSIST=0
+    // keeps one tile per workgroup
+    const char* ps_env = getenv("LSMGPU_WSC_PERSIST");
+    p.wpersist = ps_env && atoi(ps_env) == 0 ? 0u : 1u;
 
     const char* wk_env = getenv("LSMGPU_WSC_WALK");
     // Default: 8 lanes per block guessing same-shape runs (kWalkGroup) when the batch has at

@@ -1648,9 +1648,219 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
 }
 
 
+// The wide lane walk with two tiles per workgroup (LSMGPU_WSC_PERSIST=1, materialize decodes of
+// 576-thread tiles).  In wsc_walk_kernel each tile's workgroup waits for its predecessors'
+// aggregates after walking (the census: 5-7 us per tile, profiles/r05q) and only then frees the
+// CU for a second-wave tile.  Here a workgroup takes a ticket, walks that tile and publishes its
+// aggregate, takes a second ticket and walks that tile, and only then runs the look-back and the
+// per-block epilogue of both -- by which time the first tile's predecessors have long finished.
+// Every ticket is taken by a running workgroup, and a workgroup publishes both aggregates
+// before it waits on anything, so every look-back ends whatever the residency.  Each
+// workgroup makes exactly two ticket draws (the grid is ceil(tiles / 2)); draws past the last
+// tile walk nothing, and the last draw of the launch resets the counter.  The walk loop, the
+// records and the epilogue are those of wsc_walk_kernel's lane walk.
+template <uint32_t TB>
+__global__ void __launch_bounds__(TB) wsc_walk_persist_kernel(DecodeParams p) {
+  constexpr uint32_t CH = 32, kThreads = TB, kWaves = TB / kWave, kStage = CH + 1;
+  __shared__ __attribute__((aligned(16))) uint32_t stage[kThreads * kStage];
+  __shared__ uint32_t s_tile[2];
+  __shared__ uint32_t s_wave[2][kWaves][3];
+  __shared__ uint32_t s_part[kWaves][3];
+  __shared__ uint32_t s_ex[3];
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint32_t TBe = p.wtbe, ntiles = (p.nblk + TBe - 1) / TBe, draws = 2 * gridDim.x;
+  uint32_t tl[2], nn[2], KK[2], VV[2], ss[2], in_[2], ik[2], iv[2];
+#pragma unroll
+  for (uint32_t r = 0; r < 2; r++) {
+    if (tid == 0) {
+      const uint32_t t = atomicAdd(p.gcnt, 1u);
+      if (t == draws - 1) atomicExch(p.gcnt, 0u);  // the launch's last draw
+      s_tile[r] = t;
+    }
+    __syncthreads();
+    const uint32_t tile = s_tile[r];
+    tl[r] = tile;
+    nn[r] = KK[r] = VV[r] = 0;
+    ss[r] = LSMGPU_BLK_OK;
+    in_[r] = ik[r] = iv[r] = 0;
+    if (tile >= ntiles) continue;  // (uniform)
+    if (p.zero_result && tile == 0 && tid < 8)  // as wsc_walk_kernel: before anything else
+      atomicExch(reinterpret_cast<unsigned long long*>(p.result + tid), 0ull);
+    const uint32_t b = tid < TBe ? tile * TBe + tid : 0xffffffffu;
+    uint32_t n = 0, K = 0, V = 0, st = LSMGPU_BLK_OK;
+    const bool valid = b < p.nblk;
+    uint32_t* row = stage + tid * kStage;
+    uint32_t off = 0, len = 0, pos = 0;
+    if (valid) {
+      off = p.blk_off[b];
+      len = p.blk_len[b];
+    }
+    bool done = !valid || (p.ablate & 4);
+    if (valid && (uint64_t)off + len > p.data_len) {
+      st = LSMGPU_BLK_RANGE;
+      done = true;
+    }
+    const uint8_t* blk = p.data + off;
+    const uint32_t wb0 = tile * TBe + wave * 64;
+    for (uint32_t k = 0;; k++) {
+      if (__ballot(!done) == 0) break;
+      bool rec = false;
+      if (!done) {
+        do {
+          if (pos >= len) { done = true; break; }                  // iterator.go:115-118
+          if (len - pos < 10) { st = LSMGPU_BLK_TRUNC_HEADER; done = true; break; }
+          uint32_t plen, klen, vlen;
+          read_hdr_nt(blk + pos, plen, klen, vlen);                // iterator.go:121
+          if ((klen | plen) == 0) { done = true; break; }          // iterator.go:124-127
+          if (n == 0 && plen != 0) { st = LSMGPU_BLK_FIRST_PLEN; done = true; break; }
+          if (10 + plen > len) { st = LSMGPU_BLK_PREFIX_OOB; done = true; break; }
+          const uint32_t end = pos + 10 + klen + vlen;             // iterator.go:101-109
+          if (end > len) { st = LSMGPU_BLK_VALUE_OVERFLOW; done = true; break; }
+          row[n & (CH - 1)] = pos | (V << 16);
+          K += plen + klen;
+          V += vlen;
+          n++;
+          pos = end;
+          rec = true;
+        } while (false);
+      }
+      if ((k & (CH - 1)) == CH - 1) {  // whole 128-B record lines, 8 lanes per line
+        const uint64_t fl = __ballot(rec);
+        if (fl) {
+          wave_lds_fence();
+          constexpr uint32_t kPer = CH / 4;
+#pragma unroll
+          for (uint32_t q = 0; q < kPer; q++) {
+            const uint32_t L = (64 / kPer) * q + lane / kPer, part = lane % kPer;
+            if ((fl >> L) & 1ull) {
+              const uint32_t* rw = stage + (wave * 64 + L) * kStage + 4 * part;
+              uint32_t* mL = p.wmeta + (uint64_t)(wb0 + L) * p.wcap + (k - (CH - 1));
+              reinterpret_cast<uint4*>(mL)[part] = make_uint4(rw[0], rw[1], rw[2], rw[3]);
+            }
+          }
+          wave_lds_fence();
+        }
+      }
+    }
+    if (valid) row[n & (CH - 1)] = pos | (V << 16);  // the sentinel
+    const uint64_t vm = __ballot(valid);
+    wave_lds_fence();
+    {
+      constexpr uint32_t kPer = CH / 4;
+#pragma unroll
+      for (uint32_t q = 0; q < kPer; q++) {
+        const uint32_t L = (64 / kPer) * q + lane / kPer, part = lane % kPer;
+        const uint32_t nL = (uint32_t)__shfl((int)n, (int)L);
+        if ((vm >> L) & 1ull) {
+          const uint32_t* rw = stage + (wave * 64 + L) * kStage + 4 * part;
+          uint32_t* mL = p.wmeta + (uint64_t)(wb0 + L) * p.wcap + (nL & ~(CH - 1));
+          reinterpret_cast<uint4*>(mL)[part] = make_uint4(rw[0], rw[1], rw[2], rw[3]);
+        }
+      }
+    }
+    wave_lds_fence();  // the rows are read before the next tile's walk refills them
+    if (valid) {
+      uint64_t* t = p.wstat + 3ull * b;
+      t[0] = n;
+      t[1] = K;
+      t[2] = V;
+      const bool plen_b = K != pos - 10 * n - V;
+      p.wstatus[b] = st | (plen_b ? kPlenFlag : 0u);
+    }
+    // tile scan, and the tile's aggregate published at once
+    in_[r] = wave_scan_sat(n, lane);
+    ik[r] = wave_scan_sat(K, lane);
+    iv[r] = wave_scan_sat(V, lane);
+    if (lane == 63) {
+      s_wave[r][wave][0] = in_[r];
+      s_wave[r][wave][1] = ik[r];
+      s_wave[r][wave][2] = iv[r];
+    }
+    __syncthreads();
+    if (wave == 0) {
+      uint32_t tn = 0, tk = 0, tv = 0;
+      for (uint32_t w = 0; w < kWaves; w++) {
+        tn = sat_add(tn, s_wave[r][w][0]);
+        tk = sat_add(tk, s_wave[r][w][1]);
+        tv = sat_add(tv, s_wave[r][w][2]);
+      }
+      store3(p.lb + (uint64_t)tile * 8, p.tag, tn, tk, tv, lane);
+    }
+    nn[r] = n;
+    KK[r] = K;
+    VV[r] = V;
+    ss[r] = st;
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < 2; r++) {
+    const uint32_t tile = tl[r];
+    if (tile >= ntiles) continue;  // (uniform)
+    Tot part{0, 0, 0};
+    if (tile > 0 && !(p.ablate & 1)) part = lookback_partial(p.lb, tile, p.tag, tid, kThreads, p.result);
+    const uint32_t pn = wave_sum_sat(part.n), pk = wave_sum_sat(part.k), pv = wave_sum_sat(part.v);
+    if (lane == 0) {
+      s_part[wave][0] = pn;
+      s_part[wave][1] = pk;
+      s_part[wave][2] = pv;
+    }
+    __syncthreads();
+    if (wave == 0 && lane == 0) {
+      Tot ex{0, 0, 0};
+      for (uint32_t w = 0; w < kWaves; w++) {
+        ex.n = sat_add(ex.n, s_part[w][0]);
+        ex.k = sat_add(ex.k, s_part[w][1]);
+        ex.v = sat_add(ex.v, s_part[w][2]);
+      }
+      s_ex[0] = ex.n;
+      s_ex[1] = ex.k;
+      s_ex[2] = ex.v;
+    }
+    __syncthreads();
+    const uint32_t b = tid < TBe ? tile * TBe + tid : 0xffffffffu;
+    const uint32_t n = nn[r], K = KK[r], V = VV[r], st = ss[r];
+    if (b < p.nblk) {  // the epilogue of wsc_walk_kernel's lane walk
+      uint32_t on = s_ex[0], ok = s_ex[1], ov = s_ex[2];
+      for (uint32_t w = 0; w < wave; w++) {
+        on = sat_add(on, s_wave[r][w][0]);
+        ok = sat_add(ok, s_wave[r][w][1]);
+        ov = sat_add(ov, s_wave[r][w][2]);
+      }
+      const uint32_t en = sat_add(on, in_[r] - n),
+                     ek = sat_add(ok, ik[r] == 0xffffffffu ? ik[r] : ik[r] - K), ev = sat_add(ov, iv[r] - V);
+      uint64_t* bs = p.wbase + 3ull * b;
+      bs[0] = en;
+      bs[1] = ek;
+      bs[2] = ev;
+      if (p.blk_first) p.blk_first[b] = en;
+      if (p.blk_status) p.blk_status[b] = (int32_t)st;
+      if (st != LSMGPU_BLK_OK) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(p.result + 4), 1ull);
+        atomicMax(reinterpret_cast<unsigned long long*>(p.result + 3), (unsigned long long)(p.nblk - b));
+      }
+      if (b == p.nblk - 1) {  // totals of the whole batch
+        if (p.blk_first) p.blk_first[p.nblk] = (uint32_t)((uint64_t)en + n);
+        p.result[0] = (uint64_t)en + n;
+        p.result[1] = (uint64_t)ek + K;
+        p.result[2] = (uint64_t)ev + V;
+      }
+      bool fits = (uint64_t)en + n <= p.ent_cap && (uint64_t)en + n <= 0xffffffffull;
+      if (p.mode & LSMGPU_MODE_MATERIALIZE) {  // the copy's output streams
+        const uint64_t kend = (uint64_t)ek + K, vend = (uint64_t)ev + V;
+        fits = fits && (kend <= p.key_cap || !p.key_data) && (vend <= p.val_cap || !p.val_data) &&
+               kend < 0xffffffffull && vend <= 0xffffffffull;
+      }
+      if (!fits) atomicOr(reinterpret_cast<unsigned long long*>(p.result + 5), 1ull);
+    }
+    __syncthreads();  // s_part / s_ex are reused by the second tile
+  }
+}
+
 hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mid) {
   const uint32_t nblk = p.nblk;
-  if (p.wwalk == kWalkGroup && p.wlanes == 8 && p.wbidir == 2)  // 16 lanes forward + 16 backward
+  const bool persist = p.wpersist && !p.wfuse && p.wwalk != kWalkGroup && p.wwide == 576 && p.wchunk == 32 && !p.weo;
+  if (persist)
+    hipLaunchKernelGGL(wsc_walk_persist_kernel<576>, dim3(((nblk + p.wtbe - 1) / p.wtbe + 1) / 2), dim3(576), 0, s, p);
+  else if (p.wwalk == kWalkGroup && p.wlanes == 8 && p.wbidir == 2)  // 16 lanes forward + 16 backward
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroupBi, 8>), dim3((nblk + 7) / 8), dim3(256), 0, s, p);
   else if (p.wwalk == kWalkGroup && p.wlanes == 8 && p.wbidir)  // 8 lanes forward + 8 backward
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroupBi, 16>), dim3((nblk + 15) / 16), dim3(256), 0, s, p);
@@ -1690,7 +1900,7 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 256>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
   hipError_t e = hipGetLastError();
 #ifdef LSMGPU_STAMPS
-  if (e == hipSuccess && p.stamps) {  // diagnostics: the walk's per-tile timeline
+  if (e == hipSuccess && p.stamps && !persist) {  // diagnostics: the walk's per-tile timeline
     const uint32_t tb = p.wwalk == kWalkGroup ? (p.wbidir && p.wlanes == 8 ? 16 / p.wbidir : 256 / p.wlanes)
                       : (p.wwide ? p.wtbe : (p.wfuse && p.wkeep && p.wtile == 192) || p.wtile == 192 ? 192 : 256);
     const uint32_t nt = (nblk + tb - 1) / tb;

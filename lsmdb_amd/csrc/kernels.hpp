@@ -61,6 +61,7 @@ struct DecodeParams {
   uint32_t weo;             // lane walk (materialize): the walk writes key_end / val_end / view
   uint32_t weosep;          // copy, 16 lanes per entry: per-entry outputs in a separate pass
   uint32_t wtbe;            // wide lane walks: blocks per tile (<= 576; set whenever wwide is)
+  uint32_t wpersist;        // wide lane walk (materialize): two tiles per workgroup, walked back to back
   uint32_t wscopy;          // 64-lane staged group walk: each wave copies its block from LDS
   uint32_t wslot;           // 64-lane staged group walk: 0 = kStageSlot, 1 = kStageSlotSmall
   uint32_t wsub;            // group walk: odd-shaped entries re-guessed inside a round

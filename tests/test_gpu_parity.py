@@ -450,14 +450,22 @@ def test_prefix_compressed_large_output(codec, oracle, monkeypatch, path):
 
 
 @pytest.mark.parametrize("chunk,lookback", [("32", "window"), ("16", "window"), ("32", "full"),
-                                            ("16", "full")])  # (full: the default)
+                                            ("16", "full"), ("32", "persist")])  # (full: the default)
 def test_wsc_many_tiles(codec, oracle, monkeypatch, chunk, lookback):
     """The walk kernel's tiles (256 blocks, ticket order) find their output bases by decoupled
     look-back over ~40 tile records: C2 blocks plus a ragged last tile, checked against the
     oracle on every output array, three launches back to back (the ticket reset); 32- and
     16-record flush chunks; the windowed look-back and the workgroup-wide sum of every
-    predecessor's aggregate (LSMGPU_WSC_LOOKBACK=full)."""
+    predecessor's aggregate (LSMGPU_WSC_LOOKBACK=full); persist: 64-block wide tiles, two per
+    workgroup walked back to back before their look-backs (LSMGPU_WSC_PERSIST=1), whose draws
+    past the last tile and counter reset the three launches exercise."""
     monkeypatch.setenv("LSMGPU_WSC_CHUNK", chunk)
+    if lookback == "persist":
+        monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
+        monkeypatch.setenv("LSMGPU_WSC_WIDE", "1")
+        monkeypatch.setenv("LSMGPU_WSC_TBE", "1")
+        monkeypatch.setenv("LSMGPU_WSC_PERSIST", "1")
+        lookback = "full"
     monkeypatch.setenv("LSMGPU_WSC_LOOKBACK", lookback)
     c = _cols(2, 330000, seed=13)
     sst, _, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, 0, 4096)
@@ -512,7 +520,8 @@ def test_wsc_lanes_per_entry(codec, oracle, monkeypatch, lanes):
                                   "group4", "group16", "group32", "group64", "group64_copy", "group64s",
                                   "group64g", "group64g_copy", "group_sub", "group16_sub",
                                   "group_dpp", "lane_lbwin", "lane576_lbwin", "group_lbwin",
-                                  "group_bidir", "group_bidir_lbwin", "group_bidir16", "lane576tbe"])
+                                  "group_bidir", "group_bidir_lbwin", "group_bidir16", "lane576tbe",
+                                  "lane576persist"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     """Walk-scan-copy's walks (LSMGPU_WSC_WALK): one lane per block from HBM, or 8 / 4
@@ -537,7 +546,10 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
         monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
         monkeypatch.setenv("LSMGPU_WSC_WIDE", "1")
         # tbe: tiles of fewer blocks than threads (two equal waves; here 64 blocks per tile)
-        monkeypatch.setenv("LSMGPU_WSC_TBE", "1" if walk.endswith("tbe") else "0")
+        monkeypatch.setenv("LSMGPU_WSC_TBE", "1" if walk.endswith(("tbe", "persist")) else "0")
+        # persist: two tiles per workgroup walked back to back (wsc_walk_persist_kernel;
+        # materialize only, a view-only decode keeps its own kernel)
+        monkeypatch.setenv("LSMGPU_WSC_PERSIST", "1" if walk.endswith("persist") else "0")
     elif walk == "lane_viewsearch":  # view-only: owners by lane-shuffle binary search
         monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
         monkeypatch.setenv("LSMGPU_WSC_VIEWSCAN", "0")
@@ -656,8 +668,8 @@ def _block_entries(block):
     return out
 
 
-@pytest.mark.parametrize("walk", ["lane", "lane16", "lane192", "lane576", "group", "group32", "group64",
-                                  "group64g", "group_sub", "group_bidir", "group_bidir16"])
+@pytest.mark.parametrize("walk", ["lane", "lane16", "lane192", "lane576", "lane576p", "group", "group32",
+                                  "group64", "group64g", "group_sub", "group_bidir", "group_bidir16"])
 @pytest.mark.parametrize("mode", ["materialize", "view"])
 def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
     """Blocks built to defeat a header-pattern filter, decoded by every walk.  Keys and
@@ -670,6 +682,10 @@ def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
     must decode exactly as the oracle's iterator does."""
     from lsmdb_amd.codec import MODE_MATERIALIZE, MODE_VIEW
     monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
+    # lane576p: the persistent two-tile walk (LSMGPU_WSC_PERSIST=1, 64-block tiles)
+    monkeypatch.setenv("LSMGPU_WSC_PERSIST", "1" if walk == "lane576p" else "0")
+    monkeypatch.setenv("LSMGPU_WSC_TBE", "1" if walk == "lane576p" else "0")
+    walk = "lane576" if walk == "lane576p" else walk
     monkeypatch.setenv("LSMGPU_WSC_WALK", "lane" if walk in ("lane16", "lane192", "lane576")
                        else walk.replace("_sub", "").replace("_bidir16", "").replace("_bidir", ""))
     monkeypatch.setenv("LSMGPU_WSC_BIDIR", "2" if walk.endswith("_bidir16")
