@@ -439,8 +439,7 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     // (128-B) chunks
     const uint32_t cap = (max_blk_len / 10 + 1 + 31) / 32 * 32;
     const size_t meta_b = (size_t)nblk * cap * 4;
-    const size_t tri_b = ((size_t)nblk * 24 + 255) / 256 * 256;
-    const size_t wneed = meta_b + 2 * tri_b + (size_t)nblk * 4;
+    const size_t wneed = meta_b + (size_t)nblk * 32;  // records, then the 32-B descriptors
     if (wneed > c->wsc.cap) {
       HIPC(hipStreamSynchronize(c->stream));
       HIPC(c->wsc.ensure(wneed));
@@ -448,9 +447,7 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     uint8_t* w = c->wsc.as<uint8_t>();
     p.wmeta = reinterpret_cast<uint32_t*>(w);
     p.wcap = cap;
-    p.wstat = reinterpret_cast<uint64_t*>(w + meta_b);
-    p.wbase = reinterpret_cast<uint64_t*>(w + meta_b + tri_b);
-    p.wstatus = reinterpret_cast<uint32_t*>(w + meta_b + 2 * tri_b);
+    p.wdesc = reinterpret_cast<uint4*>(w + meta_b);  // (meta_b: 128-B chunks per block)
     static const uint32_t ablate =
         getenv("LSMGPU_ABLATE") ? (uint32_t)atoi(getenv("LSMGPU_ABLATE")) : 0u;
     p.ablate = ablate;

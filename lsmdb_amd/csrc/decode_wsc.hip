@@ -86,8 +86,9 @@ __device__ __forceinline__ uint32_t group_or(uint32_t x) {
 // records).  The walk stages 32 records per block in LDS and writes each chunk as one full
 // 128-B line -- 8-B stores straight from 64 lanes at 64 different blocks were evicted from L2 as
 // partial lines (4x the bytes).  Round 3: 4-B records instead of {pos | V << 16, K} (8 B).
-// p.wstatus[b] = the block's status | kPlenFlag when it holds prefix-compressed entries (the
-// walk's K exceeds the stored key bytes, stop pos - 10 n - V): the copy's header-reading path
+// The descriptor's status word (wdesc[2b].w) = the block's status | kPlenFlag when the block holds
+// prefix-compressed entries (the walk's K exceeds the stored key bytes, stop pos - 10 n - V): the
+// copy's header-reading path
 constexpr uint32_t kPlenFlag = 1u << 16;  // u32 per lane row: 32 records + 1 pad (bank spread)
 
 __device__ __forceinline__ void flush_meta(uint32_t* dst, const uint32_t* row, uint32_t cnt) {
@@ -700,14 +701,6 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
       const uint32_t sw = s_res[3][tid];
       st = sw & ~kPlenFlag;
     }
-    if (b < p.nblk && !scopy) {
-      const uint32_t sw = s_res[3][tid];
-      uint64_t* t = p.wstat + 3ull * b;
-      t[0] = n;
-      t[1] = K;
-      t[2] = V;
-      p.wstatus[b] = sw;
-    }
   } else {
     // Lane walk, records flushed cooperatively: every lane walks in lockstep (a lane that
     // stopped idles), so after iteration k with k % 32 == 31 every lane still walking holds
@@ -800,14 +793,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
         reinterpret_cast<uint4*>(mL)[part] = make_uint4(rw[0], rw[1], rw[2], rw[3]);
       }
     }
-    if (valid && !KEEP) {  // for the copy kernel (a view-only decode has none)
-      uint64_t* t = p.wstat + 3ull * b;
-      t[0] = n;
-      t[1] = K;
-      t[2] = V;
-      plen_b = K != pos - 10 * n - V;
-      p.wstatus[b] = st | (plen_b ? kPlenFlag : 0u);  // see kPlenFlag
-    }
+    if (valid && !KEEP) plen_b = K != pos - 10 * n - V;  // see kPlenFlag
   }
   // tile scan (saturating u32: a key stream past 4 GiB - 1 fails the copy's capacity check)
   const uint32_t in_ = wave_scan_sat(n, lane), ik = wave_scan_sat(K, lane),
@@ -893,11 +879,17 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
       s_cb[1][tid] = ek;
       s_cb[2][tid] = ev;
     } else {
-      if (!p.wfuse) {  // the copy kernel's bases
-        uint64_t* bs = p.wbase + 3ull * b;
-        bs[0] = en;
-        bs[1] = ek;
-        bs[2] = ev;
+      if (!p.wfuse) {  // the copy kernel's descriptor
+        uint32_t swb, offb;
+        if constexpr (GW) {
+          swb = s_res[3][tid];
+          offb = s_off[tid];
+        } else {
+          swb = st | (plen_b ? kPlenFlag : 0u);
+          offb = lane_off;
+        }
+        p.wdesc[2ull * b] = make_uint4(n, K, V, swb);
+        p.wdesc[2ull * b + 1] = make_uint4(en, ek, ev, offb);
       }
       // The per-block outputs, here for every decode (round 5; view-only decodes have no copy):
       // one thread per block writes consecutive words -- from the copy kernel, one lane per
@@ -1635,13 +1627,10 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   // the first 64 metadata records, one per lane, requested beside the per-block loads below
   // (one round trip fewer before the piece loads; records past the sentinel are never used)
   const uint32_t pre = meta[min(lane, p.wcap - 1)];
-  const uint64_t* t = p.wstat + 3ull * b;
-  const uint32_t n = uniform((uint32_t)t[0]), K = uniform((uint32_t)t[1]),
-                 V = uniform((uint32_t)t[2]);
-  const uint32_t sw = uniform(p.wstatus[b]);
-  const uint64_t* bs = p.wbase + 3ull * b;
-  const uint64_t en = uniform64(bs[0]), ek = uniform64(bs[1]), ev = uniform64(bs[2]);
-  const uint32_t off = uniform(p.blk_off[b]);
+  const uint4 d0 = p.wdesc[2ull * b], d1 = p.wdesc[2ull * b + 1];  // the walk's descriptor
+  const uint32_t n = uniform(d0.x), K = uniform(d0.y), V = uniform(d0.z), sw = uniform(d0.w);
+  const uint64_t en = uniform(d1.x), ek = uniform(d1.y), ev = uniform(d1.z);
+  const uint32_t off = uniform(d1.w);
   __shared__ uint32_t s_chunk[4][kChunkLds];  // copy_chunks' per-wave tables
   copy_block(p, b, meta, pre, n, K, V, sw, en, ek, ev, off, sub, split, lane, GlobalBytes{p.data + off},
              s_chunk[threadIdx.x >> 6], false);
@@ -1669,7 +1658,7 @@ __global__ void __launch_bounds__(TB) wsc_walk_persist_kernel(DecodeParams p) {
   __shared__ uint32_t s_ex[3];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t TBe = p.wtbe, ntiles = (p.nblk + TBe - 1) / TBe, draws = 2 * gridDim.x;
-  uint32_t tl[2], nn[2], KK[2], VV[2], ss[2], in_[2], ik[2], iv[2];
+  uint32_t tl[2], nn[2], KK[2], VV[2], ss[2], oo[2], in_[2], ik[2], iv[2];
 #pragma unroll
   for (uint32_t r = 0; r < 2; r++) {
     if (tid == 0) {
@@ -1680,7 +1669,7 @@ __global__ void __launch_bounds__(TB) wsc_walk_persist_kernel(DecodeParams p) {
     __syncthreads();
     const uint32_t tile = s_tile[r];
     tl[r] = tile;
-    nn[r] = KK[r] = VV[r] = 0;
+    nn[r] = KK[r] = VV[r] = oo[r] = 0;
     ss[r] = LSMGPU_BLK_OK;
     in_[r] = ik[r] = iv[r] = 0;
     if (tile >= ntiles) continue;  // (uniform)
@@ -1759,14 +1748,7 @@ __global__ void __launch_bounds__(TB) wsc_walk_persist_kernel(DecodeParams p) {
       }
     }
     wave_lds_fence();  // the rows are read before the next tile's walk refills them
-    if (valid) {
-      uint64_t* t = p.wstat + 3ull * b;
-      t[0] = n;
-      t[1] = K;
-      t[2] = V;
-      const bool plen_b = K != pos - 10 * n - V;
-      p.wstatus[b] = st | (plen_b ? kPlenFlag : 0u);
-    }
+    if (valid && K != pos - 10 * n - V) st |= kPlenFlag;  // (the descriptor's status word)
     // tile scan, and the tile's aggregate published at once
     in_[r] = wave_scan_sat(n, lane);
     ik[r] = wave_scan_sat(K, lane);
@@ -1790,6 +1772,7 @@ __global__ void __launch_bounds__(TB) wsc_walk_persist_kernel(DecodeParams p) {
     KK[r] = K;
     VV[r] = V;
     ss[r] = st;
+    oo[r] = off;
   }
 #pragma unroll
   for (uint32_t r = 0; r < 2; r++) {
@@ -1817,7 +1800,7 @@ __global__ void __launch_bounds__(TB) wsc_walk_persist_kernel(DecodeParams p) {
     }
     __syncthreads();
     const uint32_t b = tid < TBe ? tile * TBe + tid : 0xffffffffu;
-    const uint32_t n = nn[r], K = KK[r], V = VV[r], st = ss[r];
+    const uint32_t n = nn[r], K = KK[r], V = VV[r], sw = ss[r], st = sw & ~kPlenFlag;
     if (b < p.nblk) {  // the epilogue of wsc_walk_kernel's lane walk
       uint32_t on = s_ex[0], ok = s_ex[1], ov = s_ex[2];
       for (uint32_t w = 0; w < wave; w++) {
@@ -1827,10 +1810,8 @@ __global__ void __launch_bounds__(TB) wsc_walk_persist_kernel(DecodeParams p) {
       }
       const uint32_t en = sat_add(on, in_[r] - n),
                      ek = sat_add(ok, ik[r] == 0xffffffffu ? ik[r] : ik[r] - K), ev = sat_add(ov, iv[r] - V);
-      uint64_t* bs = p.wbase + 3ull * b;
-      bs[0] = en;
-      bs[1] = ek;
-      bs[2] = ev;
+      p.wdesc[2ull * b] = make_uint4(n, K, V, sw);
+      p.wdesc[2ull * b + 1] = make_uint4(en, ek, ev, oo[r]);
       if (p.blk_first) p.blk_first[b] = en;
       if (p.blk_status) p.blk_status[b] = (int32_t)st;
       if (st != LSMGPU_BLK_OK) {

@@ -37,12 +37,12 @@ struct DecodeParams {
   uint32_t* census;         // residency census mode (launch_decode calibration), else nullptr
   uint64_t* stamps;         // per-phase s_memtime totals (LSMGPU_STAMPS diagnostics), else nullptr
   // walk-scan-copy path (decode_wsc.hip): per-entry metadata (2 words x wcap per block),
-  // per-block {n, K, V} (u64 x 3), their exclusive scan, per-block status
+  // per-block descriptor for the copy, 32 B: wdesc[2b] = {n, K, V, status | kPlenFlag},
+  // wdesc[2b + 1] = {entry base, key base, value base, input offset} (written once, by the walk
+  // epilogue; two 16-B loads in the copy instead of five arrays)
   uint32_t* wmeta;
   uint32_t wcap;
-  uint64_t* wstat;
-  uint64_t* wbase;
-  uint32_t* wstatus;
+  uint4* wdesc;
   uint32_t wsplit;          // walk-scan-copy: waves per block in the copy (1, 2 or 4)
   uint32_t wj;              // walk-scan-copy: lanes per entry forced (8, 16), 0 = per block
   uint32_t wfuse;           // walk-scan-copy, view-only mode: the walk writes the view index
@@ -184,7 +184,7 @@ hipError_t launch_merge(const MergeParams& p, hipStream_t s);
 hipError_t launch_decode(const DecodeParams& p, uint32_t max_blk_len, int num_cus,
                          hipStream_t s, uint64_t* waves_launched);
 hipError_t launch_encode(const EncodeParams& p, int num_cus, hipStream_t s);
-// walk-scan-copy decode (blocks < 64 KiB): scratch (wmeta, wstat, wbase, wstatus) sized by
+// walk-scan-copy decode (blocks < 64 KiB): scratch (wmeta, wdesc) sized by
 // the caller; p.gcnt[0] = 0 between launches (the walk's tile ticket), p.lb tile records
 // mid (optional): an event recorded between the walk and the copy launch (kernel timing)
 hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mid = nullptr);
