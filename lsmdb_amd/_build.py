@@ -41,7 +41,11 @@ def build_lib(force: bool = False, verbose: bool = True) -> str:
     for s in SOURCES:
         obj = os.path.join(objdir, os.path.splitext(s)[0] + ".o")
         objs.append(obj)
-        cmd = flags + ["-c", "-o", obj + tag, os.path.join(CSRC, s)]
+        # a fixed compilation-unit id: clang derives __hip_cuid_* from the (per-process temporary)
+        # output path otherwise, so every rebuild would change the library's sha256 -- the key
+        # of profiles/pmc_traffic.json
+        cuid = f"-cuid=lsmgpu_{flavor}_{os.path.splitext(s)[0]}"
+        cmd = flags + [cuid, "-c", "-o", obj + tag, os.path.join(CSRC, s)]
         if verbose:
             print("[build]", " ".join(cmd), file=sys.stderr)
         jobs.append(subprocess.Popen(cmd, cwd=CSRC))
