@@ -61,12 +61,21 @@ PinRegistry& pins() {
 // page-locked bounce buffer instead: the runtime never sees the caller's address, and the call
 // stays correct whatever the runtime believes about it.  Synchronous on the stream.
 constexpr uint64_t kBounce = 8ull << 20;
-hipError_t bounce_copy(void* dst, const void* src, uint64_t n, hipMemcpyKind kind, hipStream_t s) {
+// The calling thread's bounce buffer, allocated when the thread first enters a host-memory path
+// (lsmgpu_open, lsmgpu_decode_blocks, lsmgpu_encode_blocks) rather than when a copy has already
+// been refused: a runtime short of page-locked memory at that moment could not provide it then
+// (round 5: one suite run's refused D2H reported the bounce's own allocation failure).
+uint8_t* bounce_buf() {
   thread_local uint8_t* buf = nullptr;
   if (!buf && hipHostMalloc(reinterpret_cast<void**>(&buf), kBounce, hipHostMallocPortable) != hipSuccess) {
     buf = nullptr;
-    return hipErrorOutOfMemory;
+    (void)hipGetLastError();
   }
+  return buf;
+}
+hipError_t bounce_copy(void* dst, const void* src, uint64_t n, hipMemcpyKind kind, hipStream_t s) {
+  uint8_t* const buf = bounce_buf();
+  if (!buf) return hipErrorOutOfMemory;
   hipError_t e = hipStreamSynchronize(s);  // the bounce buffer is free, earlier work is done
   for (uint64_t o = 0; o < n && e == hipSuccess; o += kBounce) {
     const uint64_t m = std::min(kBounce, n - o);
@@ -249,6 +258,7 @@ int lsmgpu_open(int device, lsmgpu_ctx** out) {
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return LSMGPU_ERR_NO_DEVICE;
   if (device < 0 || device >= ndev) return LSMGPU_ERR_NO_DEVICE;
   HIPC(hipSetDevice(device));
+  (void)bounce_buf();  // the opening thread's bounce buffer (hcopy's fallback)
   lsmgpu_ctx* c = new lsmgpu_ctx();
   c->device = device;
   hipDeviceProp_t prop;
@@ -876,6 +886,7 @@ int lsmgpu_decode_blocks(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
   if (data_len > 0xffffffffull) return LSMGPU_ERR_TOO_LARGE;
   if (mode & ~(LSMGPU_MODE_MATERIALIZE | LSMGPU_MODE_VIEW)) return LSMGPU_ERR_ARG;
   HIPC(hipSetDevice(c->device));
+  if (!data_on_device) (void)bounce_buf();  // (before any copy can be refused)
   uint32_t max_len = 0;
   for (uint64_t b = 0; b < nblk; b++) max_len = std::max(max_len, blk_len[b]);
   const bool query0 = !out->key_data && !out->key_end && !out->val_data && !out->val_end &&
@@ -1038,6 +1049,7 @@ int lsmgpu_encode_blocks(lsmgpu_ctx* c, const uint8_t* keys, const uint32_t* key
   if (query && on_device && !c) return LSMGPU_ERR_ARG;
   if (epb == 0 && block_bytes == 0) return LSMGPU_ERR_ARG;
   if (c) HIPC(hipSetDevice(c->device));
+  if (c && !on_device) (void)bounce_buf();  // (before any copy can be refused)
   SyncOnExit sync_exit;
   if (c) sync_exit.s[0] = c->stream;
   // host copies of the offset columns (needed for totals and the byte-target plan)
