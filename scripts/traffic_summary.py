@@ -19,7 +19,7 @@ import json
 import os
 import sys
 
-PIPELINE = ("lsmgpu::decode", "wsc_walk_kernel", "wsc_copy_kernel", "wsc_carry_kernel", "Tri64",
+PIPELINE = ("lsmgpu::decode", "wsc_walk_kernel", "wsc_walk_persist_kernel", "wsc_copy_kernel", "wsc_carry_kernel", "Tri64",
             "tile_decode_kernel", "fsw_kernel", "fsc_kernel")
 # not part of a materialize decode: the view-only walk (kWalkLaneView = 3) that bench.py's
 # walk_fetch_bytes runs once to price the walk
