@@ -12,6 +12,7 @@ SOURCES = ["api.hip", "decode.hip", "decode_wsc.hip", "encode.hip", "open_tables
 HEADERS = ["codec_common.hpp", "decode_common.hpp", "kernels.hpp", "pin_registry.hpp",
            os.path.join("..", "..", "include", "lsmgpu.h")]
 ARCH = os.environ.get("LSMGPU_ARCH", "gfx950")
+FLAGS = ("hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall")
 
 
 def _stale(target: str, deps: list[str]) -> bool:
@@ -21,13 +22,21 @@ def _stale(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def compile_cmd(flags: list[str], src: str, out: str, flavor: str) -> list[str]:
+    """hipcc line for one source.  A fixed compilation-unit id: clang derives __hip_cuid_* from
+    the (per-process temporary) output path otherwise, so every rebuild would change the
+    library's sha256 -- the key of profiles/pmc_traffic.json (tests/test_build.py)."""
+    cuid = f"-cuid=lsmgpu_{flavor}_{os.path.splitext(src)[0]}"
+    return flags + [cuid, "-c", "-o", out, os.path.join(CSRC, src)]
+
+
 def build_lib(force: bool = False, verbose: bool = True) -> str:
     """Each source compiled to its own object in parallel, then one link.  Every flavor (the
     product library, the LSMGPU_BUILD_STAMPS diagnostic one) has its own object directory, and
     objects and the library are written to temporary names renamed into place, so two builds at
     once (two bench ranks, two test processes) never read each other's half-written files."""
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
-    flags = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall"]
+    flags = list(FLAGS)
     lib, flavor = LIB, "default"
     if os.environ.get("LSMGPU_BUILD_STAMPS"):  # diagnostic build: per-phase s_memtime stamps
         flags.append("-DLSMGPU_STAMPS")
@@ -41,11 +50,7 @@ def build_lib(force: bool = False, verbose: bool = True) -> str:
     for s in SOURCES:
         obj = os.path.join(objdir, os.path.splitext(s)[0] + ".o")
         objs.append(obj)
-        # a fixed compilation-unit id: clang derives __hip_cuid_* from the (per-process temporary)
-        # output path otherwise, so every rebuild would change the library's sha256 -- the key
-        # of profiles/pmc_traffic.json
-        cuid = f"-cuid=lsmgpu_{flavor}_{os.path.splitext(s)[0]}"
-        cmd = flags + [cuid, "-c", "-o", obj + tag, os.path.join(CSRC, s)]
+        cmd = compile_cmd(flags, s, obj + tag, flavor)
         if verbose:
             print("[build]", " ".join(cmd), file=sys.stderr)
         jobs.append(subprocess.Popen(cmd, cwd=CSRC))
