@@ -27,8 +27,12 @@ extern "C" {
 /* 2 (round 4): size queries (decode with every output pointer NULL, encode with out == NULL),
  * LSMGPU_ERR_CORRUPT, stream probe kinds 4-7 and its argument checks.
  * 3 (round 5): lsmgpu_host_register is refcounted per page segment (overlapping and re-used
- * ranges), LSMGPU_ERR_HOST_PINNED, unregister of an unknown pointer is LSMGPU_ERR_ARG. */
-#define LSMGPU_ABI_VERSION 3
+ * ranges), LSMGPU_ERR_HOST_PINNED, unregister of an unknown pointer is LSMGPU_ERR_ARG.
+ * 4 (round 6): the library never page-locks caller memory: pageable host buffers are staged
+ * through page-locked buffers it owns (hipHostMalloc, per ctx), runtime-pinned ones are DMA'd
+ * directly; lsmgpu_host_alloc / lsmgpu_host_free hand out such memory; lsmgpu_host_register /
+ * unregister keep their argument and error rules but pin nothing. */
+#define LSMGPU_ABI_VERSION 4
 
 /* ---- call status ---- */
 #define LSMGPU_OK 0
@@ -132,23 +136,22 @@ int lsmgpu_decode_blocks(lsmgpu_ctx* ctx, const uint8_t* data, uint64_t data_len
                          uint64_t nblk, int mode, lsmgpu_decoded* out);
 
 /* Host-memory calls (data_on_device = 0) with blocks sorted by offset are pipelined: chunks of
- * ~64 MiB (LSMGPU_HOST_CHUNK) are copied in, decoded and copied out on three streams at once.
- * DMA runs at PCIe rate only from page-locked memory: pin the .sst bytes (an mmap -- read-only
- * mappings are pinned read-only -- or LoadToRAM's heap buffer, table.go:117-123,329-338) and
- * large output arrays with lsmgpu_host_register, unpin with lsmgpu_host_unregister(p) (the same
- * pointer) before the memory is freed or unmapped.
- * Pinning is page-granular: the whole pages inside the range are pinned, its partial first and
- * last pages are not (they may hold other allocations' bytes; copies of those < 2 pages are
- * staged by the runtime).  The library keeps one process-wide registry of page-aligned
- * segments, each pinned once: a range pins only its pages no earlier registration covers and
- * references every segment it overlaps, so ranges may share pages, nest, repeat and come back
- * at re-used addresses; a segment is unpinned when its last range is unregistered.  Every host
- * copy the library makes is cut at segment borders.  Register / unregister are thread-safe.
- * Returns LSMGPU_ERR_HOST_PINNED (nothing registered) for memory already page-locked outside
- * the library, and LSMGPU_ERR_HIP when the OS refuses (e.g. RLIMIT_MEMLOCK): the host calls then
- * work on the memory as it is, staged by the runtime.  lsmgpu_host_unregister of a pointer with
- * no registration returns LSMGPU_ERR_ARG.  Unregister only when no call using memory in the same
- * pages is running. */
+ * ~32 MiB (LSMGPU_HOST_CHUNK) are copied in, decoded and copied out on three streams at once.
+ * Host memory is never page-locked by the library (ABI 4).  Memory the HIP runtime already
+ * knows as page-locked -- lsmgpu_host_alloc, hipHostMalloc, torch's pinned allocator -- is DMA'd
+ * directly at PCIe rate; any other host memory (a Go heap buffer under LoadToRAM,
+ * table.go:117-123,329-338; an mmap'd .sst, y/mmap.go:11-21; pageable output arrays) is staged
+ * through page-locked buffers the ctx owns, filled and drained by memcpy on a small per-ctx
+ * thread pool (LSMGPU_COPY_THREADS, default min(8, hardware threads)).  So a caller that wants
+ * one copy of a table end to end reads the file into lsmgpu_host_alloc memory.
+ * Every host call has finished all DMA into or out of caller memory when it returns. */
+int lsmgpu_host_alloc(lsmgpu_ctx* ctx, uint64_t bytes, void** out);  /* hipHostMalloc, portable */
+int lsmgpu_host_free(lsmgpu_ctx* ctx, void* p);  /* p NULL: no-op; ctx may be NULL (any device) */
+
+/* ABI 3 compatibility: records a range the caller will pass (nothing is page-locked).  Returns
+ * LSMGPU_ERR_HOST_PINNED (nothing recorded) for memory the runtime already knows as page-locked
+ * (it needs no registration); lsmgpu_host_unregister(p) drops the latest record at p and returns
+ * LSMGPU_ERR_ARG if there is none.  Thread-safe. */
 int lsmgpu_host_register(lsmgpu_ctx* ctx, void* p, uint64_t bytes);
 int lsmgpu_host_unregister(lsmgpu_ctx* ctx, void* p);
 

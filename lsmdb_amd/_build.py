@@ -9,7 +9,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "lsmdb_amd", "csrc")
 LIB = os.path.join(ROOT, "lsmdb_amd", "liblsmgpu.so")
 SOURCES = ["api.hip", "decode.hip", "decode_wsc.hip", "encode.hip", "open_tables.hip", "merge.hip", "bloom.hip", "probe.hip"]
-HEADERS = ["codec_common.hpp", "decode_common.hpp", "kernels.hpp", "pin_registry.hpp",
+HEADERS = ["codec_common.hpp", "decode_common.hpp", "kernels.hpp", "host_io.hpp", "copy_pool.hpp",
            os.path.join("..", "..", "include", "lsmgpu.h")]
 ARCH = os.environ.get("LSMGPU_ARCH", "gfx950")
 FLAGS = ("hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall")
@@ -32,15 +32,17 @@ def compile_cmd(flags: list[str], src: str, out: str, flavor: str) -> list[str]:
 
 def build_lib(force: bool = False, verbose: bool = True) -> str:
     """Each source compiled to its own object in parallel, then one link.  Every flavor (the
-    product library, the LSMGPU_BUILD_STAMPS diagnostic one) has its own object directory, and
+    product library, the LSMGPU_BUILD_DIAG diagnostic one) has its own object directory, and
     objects and the library are written to temporary names renamed into place, so two builds at
     once (two bench ranks, two test processes) never read each other's half-written files."""
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
     flags = list(FLAGS)
     lib, flavor = LIB, "default"
-    if os.environ.get("LSMGPU_BUILD_STAMPS"):  # diagnostic build: per-phase s_memtime stamps
-        flags.append("-DLSMGPU_STAMPS")
-        lib, flavor = LIB.replace("liblsmgpu.so", "liblsmgpu_stamps.so"), "stamps"
+    # the diagnostic build (kernels.hpp): the rejected variants, A/B knobs, timing ablations and
+    # per-phase s_memtime stamps; the product library compiles only the adopted paths
+    if os.environ.get("LSMGPU_BUILD_DIAG") or os.environ.get("LSMGPU_BUILD_STAMPS"):
+        flags.append("-DLSMGPU_DIAG")
+        lib, flavor = LIB.replace("liblsmgpu.so", "liblsmgpu_diag.so"), "diag"
     if not force and not _stale(lib, deps):
         return lib
     objdir = os.path.join(ROOT, "lsmdb_amd", "build", flavor)

@@ -75,6 +75,8 @@ EXPORTED_SYMBOLS = (
     "lsmgpu_stream_probe_async",
     "lsmgpu_host_register",
     "lsmgpu_host_unregister",
+    "lsmgpu_host_alloc",
+    "lsmgpu_host_free",
 )
 
 COMPACT_BLOOM = 1
@@ -265,6 +267,11 @@ def _load() -> ctypes.CDLL:
     lib.lsmgpu_host_register.restype = c_int
     lib.lsmgpu_host_unregister.argtypes = [c_void_p, c_void_p]
     lib.lsmgpu_host_unregister.restype = c_int
+    if hasattr(lib, "lsmgpu_host_alloc"):  # (ABI >= 4; diagnostics may load an older build)
+        lib.lsmgpu_host_alloc.argtypes = [c_void_p, c_uint64, POINTER(c_void_p)]
+        lib.lsmgpu_host_alloc.restype = c_int
+        lib.lsmgpu_host_free.argtypes = [c_void_p, c_void_p]
+        lib.lsmgpu_host_free.restype = c_int
     return lib
 
 

@@ -173,17 +173,35 @@ class Codec:
         check(lib().lsmgpu_stream_probe_async(self._ctx, kind, _ptr(src), _ptr(dst), nbytes,
                                               wg_per_cu), "stream_probe_async")
 
-    # -- page-locked host memory (DMA at PCIe rate for the host-buffer calls)
+    # -- host memory.  Pageable arrays are staged through the ctx's own page-locked buffers;
+    # host_alloc memory is DMA'd directly (include/lsmgpu.h, ABI 4)
+    def host_alloc(self, nbytes: int) -> np.ndarray:
+        """A u8 array of nbytes in page-locked memory (lsmgpu_host_alloc), freed with the array."""
+        import weakref
+        p = c_void_p()
+        check(lib().lsmgpu_host_alloc(self._ctx, max(int(nbytes), 1), byref(p)), "host_alloc")
+        buf = (ctypes.c_uint8 * max(int(nbytes), 1)).from_address(p.value)
+        weakref.finalize(buf, lib().lsmgpu_host_free, None, p.value)
+        return np.frombuffer(buf, np.uint8, count=int(nbytes))
+
     def host_register(self, arr) -> None:
-        """Pins a host numpy array (an mmap'd .sst, an output array) until host_unregister."""
+        """ABI-3 compatibility: records the array's range (nothing is page-locked)."""
         check(lib().lsmgpu_host_register(self._ctx, _ptr(arr), arr.nbytes), "host_register")
 
     def host_unregister(self, arr) -> None:
         check(lib().lsmgpu_host_unregister(self._ctx, _ptr(arr)), "host_unregister")
 
     # -- decode, host buffers (table.Table path)
+    def _host_zeros(self, n: int, dtype, pinned: bool) -> np.ndarray:
+        if not pinned:
+            return np.zeros(n, dtype=dtype)
+        a = self.host_alloc(max(n, 1) * np.dtype(dtype).itemsize).view(dtype)[:n]
+        a[:] = 0
+        return a
+
     def decode_host(self, data, blk_off: np.ndarray, blk_len: np.ndarray,
-                    mode: int = MODE_MATERIALIZE | MODE_VIEW) -> HostDecoded:
+                    mode: int = MODE_MATERIALIZE | MODE_VIEW, pinned_out: bool = False) -> HostDecoded:
+        """pinned_out: the output arrays live in host_alloc memory (DMA'd directly, no staging)."""
         buf = _np_u8(data)
         off = np.ascontiguousarray(blk_off, dtype=np.uint32)
         ln = np.ascontiguousarray(blk_len, dtype=np.uint32)
@@ -194,13 +212,14 @@ class Codec:
         # mode also materializes, so the HostDecoded accessors work
         eff = mode if mode == MODE_VIEW else mode | MODE_MATERIALIZE
         for _attempt in range(2):
-            kd = np.zeros(key_cap, dtype=np.uint8)
-            vd = np.zeros(val_cap, dtype=np.uint8)
-            ke = np.zeros(ent_cap, dtype=np.uint32)
-            ve = np.zeros(ent_cap, dtype=np.uint32)
-            vw = np.zeros(ent_cap, dtype=np.uint64) if mode & MODE_VIEW else None
-            bf = np.zeros(nblk + 1, dtype=np.uint32)
-            bs = np.zeros(max(nblk, 1), dtype=np.int32)
+            z = lambda n, t: self._host_zeros(n, t, pinned_out)  # noqa: E731
+            kd = z(key_cap, np.uint8)
+            vd = z(val_cap, np.uint8)
+            ke = z(ent_cap, np.uint32)
+            ve = z(ent_cap, np.uint32)
+            vw = z(ent_cap, np.uint64) if mode & MODE_VIEW else None
+            bf = z(nblk + 1, np.uint32)
+            bs = z(max(nblk, 1), np.int32)
             d = LsmgpuDecoded()
             d.key_data, d.key_cap, d.key_end = _ptr(kd), kd.size, _ptr(ke)
             d.val_data, d.val_cap, d.val_end = _ptr(vd), vd.size, _ptr(ve)

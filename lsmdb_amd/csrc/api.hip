@@ -9,15 +9,15 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
-#include <shared_mutex>
 #include <vector>
 
 #include <unistd.h>
 
 #include "../../include/lsmgpu.h"
 #include "kernels.hpp"
-#include "pin_registry.hpp"
+#include "host_io.hpp"
 
 using namespace lsmgpu;
 
@@ -50,112 +50,15 @@ inline uint32_t rd_be32(const uint8_t* b) {
   return ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
 }
 
-// the process's page-locked segments (lsmgpu_host_register; pin_registry.hpp)
-PinRegistry& pins() {
-  static PinRegistry r((uintptr_t)sysconf(_SC_PAGESIZE));
-  return r;
-}
-
-// A host copy HIP refuses (hipErrorInvalidValue: its pinned-memory bookkeeping disagrees with the
-// pages -- seen on buffers re-registered at re-used heap addresses) is done through this thread's
-// page-locked bounce buffer instead: the runtime never sees the caller's address, and the call
-// stays correct whatever the runtime believes about it.  Synchronous on the stream.
-constexpr uint64_t kBounce = 8ull << 20;
-// The calling thread's bounce buffer, allocated when the thread first enters a host-memory path
-// (lsmgpu_open, lsmgpu_decode_blocks, lsmgpu_encode_blocks) rather than when a copy has already
-// been refused: a runtime short of page-locked memory at that moment could not provide it then
-// (round 5: one suite run's refused D2H reported the bounce's own allocation failure).
-uint8_t* bounce_buf() {
-  thread_local uint8_t* buf = nullptr;
-  if (!buf && hipHostMalloc(reinterpret_cast<void**>(&buf), kBounce, hipHostMallocPortable) != hipSuccess) {
-    buf = nullptr;
-    (void)hipGetLastError();
-  }
-  return buf;
-}
-hipError_t bounce_copy(void* dst, const void* src, uint64_t n, hipMemcpyKind kind, hipStream_t s) {
-  uint8_t* const buf = bounce_buf();
-  if (!buf) return hipErrorOutOfMemory;
-  hipError_t e = hipStreamSynchronize(s);  // the bounce buffer is free, earlier work is done
-  for (uint64_t o = 0; o < n && e == hipSuccess; o += kBounce) {
-    const uint64_t m = std::min(kBounce, n - o);
-    if (kind == hipMemcpyHostToDevice) {
-      std::memcpy(buf, static_cast<const uint8_t*>(src) + o, m);
-      e = hipMemcpyAsync(static_cast<uint8_t*>(dst) + o, buf, m, kind, s);
-      if (e == hipSuccess) e = hipStreamSynchronize(s);
-    } else {
-      e = hipMemcpyAsync(buf, static_cast<const uint8_t*>(src) + o, m, kind, s);
-      if (e == hipSuccess) e = hipStreamSynchronize(s);
-      if (e == hipSuccess) std::memcpy(static_cast<uint8_t*>(dst) + o, buf, m);
-    }
-  }
-  return e;
-}
-
-// hipMemcpyAsync between HBM and a host range, cut where pinned segments begin and end: HIP serves
-// a copy from the registration its first byte lies in and rejects one that runs past that
-// registration's end (a buffer whose edge pages another caller pinned, or a neighbour's).  Every
-// host copy of the library goes through here; a piece HIP refuses goes through bounce_copy.
-// hcopy's account of a failed piece (its range, HIP's view of the host pointer), joined to the
-// next reported HIP error (lsmgpu_last_error)
-static thread_local char t_hcopy_detail[160] = "";
-hipError_t hcopy(void* dst, const void* src, uint64_t n, hipMemcpyKind kind, hipStream_t s) {
-  if (!n) return hipSuccess;
-  const bool h2d = kind == hipMemcpyHostToDevice;
-  const uintptr_t h = (uintptr_t)(h2d ? src : dst);
-  std::vector<PinRegistry::Range> pc;
-  // shared: copies run concurrently; a re-cut of segments (unregister) waits for them and keeps
-  // new ones out until the re-pin is done
-  std::shared_lock<std::shared_mutex> g(pins().mu());
-  pins().pieces(h, n, &pc);
-  for (const auto& r : pc) {
-    const uint64_t o = r.first - h, m = r.second - r.first;
-    void* d = static_cast<uint8_t*>(dst) + o;
-    const void* q = static_cast<const uint8_t*>(src) + o;
-    hipError_t e = hipMemcpyAsync(d, q, m, kind, s);
-    // (any refusal, not only hipErrorInvalidValue: a sporadic host-path ERR_HIP in round 5's
-    // suite (encode_blocks from numpy memory after register / unregister cycles at re-used
-    // addresses) named no call; the bounce does not depend on what the runtime believes)
-    if (e != hipSuccess) {
-      static const bool dbg = getenv("LSMGPU_DEBUG_ERR") != nullptr;
-      if (dbg)
-        fprintf(stderr, "lsmgpu: hcopy %s host piece [%#lx, %#lx) of [%#lx, %#lx) refused (%s): bounce\n",
-                h2d ? "H2D" : "D2H", (unsigned long)r.first, (unsigned long)r.second,
-                (unsigned long)h, (unsigned long)(h + n), hipGetErrorString(e));
-      (void)hipGetLastError();
-      e = bounce_copy(d, q, m, kind, s);
-    }
-    if (e != hipSuccess) {
-      hipPointerAttribute_t a{};
-      const hipError_t ea = hipPointerGetAttributes(&a, reinterpret_cast<const void*>(r.first));
-      snprintf(t_hcopy_detail, sizeof(t_hcopy_detail), "%s piece [%#lx, %#lx) of [%#lx, %#lx), %zu pieces, "
-               "host pointer type %d (query %d)", h2d ? "H2D" : "D2H", (unsigned long)r.first,
-               (unsigned long)r.second, (unsigned long)h, (unsigned long)(h + n), pc.size(),
-               ea == hipSuccess ? (int)a.type : -1, (int)ea);
-      (void)hipGetLastError();
-      return e;
-    }
-  }
-  return hipSuccess;
-}
-
-// Memory page-locked outside this library (hipHostMalloc, a caller's hipHostRegister): the
-// runtime reports it as host memory.  Caller holds the registry lock; ptrs inside our own
-// segments are not foreign.
-bool pinned_elsewhere(const void* p) {
-  hipPointerAttribute_t a{};
-  const hipError_t e = hipPointerGetAttributes(&a, p);
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  return a.type == hipMemoryTypeHost;
-}
-
-// LSMGPU_DEBUG_PIN=1: every pin / unpin of a segment on stderr (diagnostics)
-bool debug_pin() {
-  static const bool on = getenv("LSMGPU_DEBUG_PIN") != nullptr;
-  return on;
+// Ranges callers declared with lsmgpu_host_register (ABI 3 compatibility: bookkeeping only,
+// nothing is page-locked -- host_io.hpp)
+struct HostRanges {
+  std::mutex mu;
+  std::multimap<uintptr_t, uint64_t> r;
+};
+HostRanges& host_ranges() {
+  static HostRanges h;
+  return h;
 }
 
 // Synchronizes the given streams when the scope ends, on every return path: a call that returns
@@ -201,20 +104,35 @@ struct lsmgpu_ctx {
   // streams, per-slot device buffers and events, pinned per-chunk result words
   static constexpr int kSlots = 3;
   hipStream_t s_in = nullptr, s_out = nullptr;
+  struct Drain {  // a staged output piece: pin_out[at, at + n) -> caller dst, after out_done
+    void* dst;
+    uint64_t at, n;
+  };
   struct Slot {
     DevBuf data, off, len, kd, ke, vd, ve, view, bf, bs, res;
+    PinnedBuf pin_in, pin_out;  // staging of the chunk's input / outputs (pageable callers)
+    std::vector<Drain> drains;  // outputs of the slot's chunk still to drain from pin_out
+    bool in_used = false;       // in_done guards a DMA out of pin_in
     hipEvent_t in_done = nullptr, dec_done = nullptr, out_done = nullptr;
   } slot[kSlots];
   uint64_t* h_chunk_res = nullptr;  // pinned, 8 u64 per slot
+  // every other host <-> HBM copy: direct DMA for runtime-pinned memory, else staged (host_io.hpp)
+  CopyPool* pool = nullptr;
+  Stager* stage = nullptr;
 };
+
+namespace {
+inline hipError_t hcopy(lsmgpu_ctx* c, void* dst, const void* src, uint64_t n, hipMemcpyKind kind,
+                        hipStream_t s) {
+  return kind == hipMemcpyHostToDevice ? c->stage->h2d(dst, src, n, s) : c->stage->d2h(dst, src, n, s);
+}
+}  // namespace
 
 // The failing HIP call and its error, kept per thread for lsmgpu_last_error; LSMGPU_DEBUG_ERR=1
 // also prints it on stderr
 static thread_local char t_last_error[256] = "";
 static void report_hip_error(const char* what, hipError_t e, int line) {
-  snprintf(t_last_error, sizeof(t_last_error), "%s -> %s (api.hip:%d)%s%s", what, hipGetErrorString(e), line,
-           t_hcopy_detail[0] ? ": " : "", t_hcopy_detail);
-  t_hcopy_detail[0] = 0;
+  snprintf(t_last_error, sizeof(t_last_error), "%s -> %s (api.hip:%d)", what, hipGetErrorString(e), line);
   static const bool on = getenv("LSMGPU_DEBUG_ERR") != nullptr;
   if (on) fprintf(stderr, "lsmgpu: %s\n", t_last_error);
 }
@@ -258,9 +176,10 @@ int lsmgpu_open(int device, lsmgpu_ctx** out) {
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return LSMGPU_ERR_NO_DEVICE;
   if (device < 0 || device >= ndev) return LSMGPU_ERR_NO_DEVICE;
   HIPC(hipSetDevice(device));
-  (void)bounce_buf();  // the opening thread's bounce buffer (hcopy's fallback)
   lsmgpu_ctx* c = new lsmgpu_ctx();
   c->device = device;
+  c->pool = new CopyPool(copy_threads());
+  c->stage = new Stager(c->pool);
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->num_cus = prop.multiProcessorCount;
@@ -293,10 +212,15 @@ void lsmgpu_close(lsmgpu_ctx* c) {
                     &c->cp_mke, &c->cp_mve, &c->cp_tf, &c->cp_tb, &c->cp_to,
                     &c->cp_out, &c->cp_flags, &c->cp_scratch};
   for (DevBuf* b : bufs) b->release();
+  if (c->stage) c->stage->release();
+  delete c->stage;
+  delete c->pool;
   for (auto& sl : c->slot) {
     DevBuf* sb[] = {&sl.data, &sl.off, &sl.len, &sl.kd, &sl.ke, &sl.vd, &sl.ve, &sl.view,
                     &sl.bf, &sl.bs, &sl.res};
     for (DevBuf* b : sb) b->release();
+    sl.pin_in.release();
+    sl.pin_out.release();
     for (hipEvent_t* e : {&sl.in_done, &sl.dec_done, &sl.out_done})
       if (*e) (void)hipEventDestroy(*e);
   }
@@ -396,6 +320,50 @@ static void next_tag(lsmgpu_ctx* c, uint64_t nblk) {
   (void)nblk;
 }
 
+#ifdef LSMGPU_DIAG
+}  // extern "C"
+// The diagnostic build's A/B knobs over the rejected variants: LSMGPU_ABLATE,
+// LSMGPU_WSC_{SPLIT,J,CHUNK,VIEWKEEP,TILE,ALIGN,LOOKBACK,BIDIR,PADLDS,TBE,PERSIST,EOSEP,EO,
+// STAGECOPY,SUB,DPP,VIEWSCAN,SLOT} and LSMGPU_WSC_WALK=group2..group64
+static void decode_diag_knobs(DecodeParams& p, uint64_t nblk, uint64_t cus, uint32_t max_blk_len,
+                              const char* wk_env) {
+  auto env = [](const char* n) { return getenv(n); };
+  p.ablate = env("LSMGPU_ABLATE") ? (uint32_t)atoi(env("LSMGPU_ABLATE")) : 0u;
+  if (const char* v = env("LSMGPU_WSC_SPLIT")) {
+    const uint32_t sp = (uint32_t)atoi(v);
+    p.wsplit = (sp == 2 || sp == 4) ? sp : 1u;
+  }
+  p.wj = env("LSMGPU_WSC_J") ? (uint32_t)atoi(env("LSMGPU_WSC_J")) : 0u;
+  if (p.wj != 8 && p.wj != 16) p.wj = 0;
+  if (const char* v = env("LSMGPU_WSC_CHUNK")) p.wchunk = atoi(v) == 16 ? 16u : 32u;
+  if (const char* v = env("LSMGPU_WSC_VIEWKEEP")) p.wkeep = atoi(v) == 0 ? 0u : 1u;
+  if (const char* v = env("LSMGPU_WSC_TILE")) p.wtile = atoi(v) == 192 ? 192u : 256u;
+  p.walign = env("LSMGPU_WSC_ALIGN") ? (uint32_t)atoi(env("LSMGPU_WSC_ALIGN")) : 0u;
+  if (const char* v = env("LSMGPU_WSC_LOOKBACK")) p.wlbfull = strcmp(v, "window") == 0 ? 0u : 1u;
+  if (const char* v = env("LSMGPU_WSC_BIDIR")) p.wbidir = (uint32_t)std::min(std::max(atoi(v), 0), 2);
+  p.wpad = env("LSMGPU_WSC_PADLDS") ? (uint32_t)atoi(env("LSMGPU_WSC_PADLDS")) : 0u;
+  if (p.wwide && env("LSMGPU_WSC_TBE") && atoi(env("LSMGPU_WSC_TBE")) == 0) p.wtbe = 576u;
+  if (const char* v = env("LSMGPU_WSC_PERSIST")) p.wpersist = atoi(v) == 0 ? 0u : 1u;
+  if (wk_env && strncmp(wk_env, "group", 5) == 0) {
+    const int l = atoi(wk_env + 5);  // "group" alone: 8 lanes
+    p.wlanes = l == 2 || l == 4 || l == 16 || l == 32 || l == 64 ? (uint32_t)l : 8u;
+  }
+  p.weosep = env("LSMGPU_WSC_EOSEP") && atoi(env("LSMGPU_WSC_EOSEP")) == 1 ? 1u : 0u;
+  p.weo = p.wwalk == kWalkLane && !p.wfuse && env("LSMGPU_WSC_EO") && atoi(env("LSMGPU_WSC_EO")) == 1 ? 1u : 0u;
+  const char* sc = env("LSMGPU_WSC_STAGECOPY");
+  p.wscopy = p.wwalk == kWalkGroup && p.wlanes == 64 && !p.wfuse && !(sc && atoi(sc) == 0);
+  p.wsub = env("LSMGPU_WSC_SUB") && atoi(env("LSMGPU_WSC_SUB")) == 1 ? 1u : 0u;
+  p.wdpp = env("LSMGPU_WSC_DPP") && atoi(env("LSMGPU_WSC_DPP")) == 1 ? 1u : 0u;
+  if (const char* v = env("LSMGPU_WSC_VIEWSCAN")) p.wview = atoi(v) == 0 ? 0u : 1u;
+  const char* sl = env("LSMGPU_WSC_SLOT");
+  p.wslot = sl && sl[0] == 's' ? 1u : (sl && sl[0] == 'n' ? 2u : 0u);
+  (void)nblk;
+  (void)cus;
+  (void)max_blk_len;
+}
+extern "C" {
+#endif
+
 int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t data_len,
                                const uint32_t* d_blk_off, const uint32_t* d_blk_len,
                                uint64_t nblk, uint32_t max_blk_len, int mode,
@@ -458,126 +426,46 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     p.wmeta = reinterpret_cast<uint32_t*>(w);
     p.wcap = cap;
     p.wdesc = reinterpret_cast<uint4*>(w + meta_b);  // (meta_b: 128-B chunks per block)
-    static const uint32_t ablate =
-        getenv("LSMGPU_ABLATE") ? (uint32_t)atoi(getenv("LSMGPU_ABLATE")) : 0u;
-    p.ablate = ablate;
-    // big blocks: several waves copy one block (more bytes in flight per block); LSMGPU_WSC_SPLIT
-    const char* sp_env = getenv("LSMGPU_WSC_SPLIT");
-    uint32_t split = max_blk_len > 8192 ? 2u : 1u;  // measured: C5 1.25 -> 1.09 ms at 2
-    if (sp_env) split = (uint32_t)atoi(sp_env);
-    p.wsplit = (split == 2 || split == 4) ? split : 1u;
-    const char* j_env = getenv("LSMGPU_WSC_J");  // A/B: lanes per entry in the copy
-    p.wj = j_env ? (uint32_t)atoi(j_env) : 0u;
-    if (p.wj != 8 && p.wj != 16) p.wj = 0;
-    // view-only decode finishes inside the walk when there are >= 2 walk tiles (256 blocks)
-    // per CU; with fewer, the tile epilogues run on too few workgroups and the copy launch wins
-    // (measured: C2 1 GiB 0.413 -> 0.323 ms fused; C4 64 MiB, 21 tiles: 0.085 -> 0.165 ms).
-    // LSMGPU_WSC_VIEWFUSE=1 / 0 forces it on / off.
-    const char* vf_env = getenv("LSMGPU_WSC_VIEWFUSE");
-    const bool fuse = vf_env ? atoi(vf_env) != 0 : nblk >= 512ull * (uint64_t)c->num_cus;
-    p.wfuse = !(mode & LSMGPU_MODE_MATERIALIZE) && fuse;
-    // lane walk: 32-record (128-B) or 16-record (64-B) flushes.  16 halves the walk's LDS (8
-    // workgroups per CU instead of 4, so C2's 1,041 tiles at 2^30 B are all resident), but
-    // flushes twice as often; same-box A/Bs split (profiles/r04b: walk 0.232 vs 0.226 ms for
-    // 16; profiles/r04d: 0.229 vs 0.236 for 32), so 32 stays the default
-    const char* ch_env = getenv("LSMGPU_WSC_CHUNK");
-    p.wchunk = ch_env && atoi(ch_env) == 16 ? 16u : 32u;
-    // view-only lane walk: the records stay in LDS (kWalkLaneView); LSMGPU_WSC_VIEWKEEP=0 flushes
-    // them to p.wmeta and re-reads them in the owner-map epilogue instead (round 3)
-    const char* vk_env = getenv("LSMGPU_WSC_VIEWKEEP");
-    p.wkeep = vk_env && atoi(vk_env) == 0 ? 0u : 1u;
-    const char* wt_env = getenv("LSMGPU_WSC_TILE");  // A/B: lane-walk workgroup of 192 / 256
-    p.wtile = wt_env && atoi(wt_env) == 192 ? 192u : 256u;
-    // lane walks: 576-block tiles (9 waves, 2 workgroups per CU) when 256-block ones (4 per CU,
-    // LDS-bound) would not all be resident at once and 576-block ones would -- a second wave of
-    // tiles walks its ~31 dependent hops at low load (C2 2^30 B: 1,041 tiles of 256 for 1,024
-    // slots; same box: walk 0.2296 -> 0.210 ms, view 0.258 -> 0.233 ms, decode 1,365 -> 1,400
-    // GiB/s, profiles/r05c, r05d, r05e).  With every 256-block tile resident the wide tile is
-    // slightly slower (walk 0.2005 vs 0.2036 ms).  LSMGPU_WSC_WIDE=0 / 1 forces it off / on.
-    // copy: LSMGPU_WSC_ALIGN=1 writes the key and value streams of blocks of <= 63 entries as
-    // aligned 16-B chunks per entry group (copy_entries_aligned), =2 as dense aligned chunks over
-    // both streams (copy_chunks).  Off by default: same-box A/B, =1 is slower
-    // (C2 copy 0.617-0.763 vs 0.495 ms) -- it does not cut the L2 write requests (TCP_TCC_WRITE_REQ
-    // 19.6 M vs 19.9 M per launch) and doubles the VALU / vector-read instructions
-    const char* al_env = getenv("LSMGPU_WSC_ALIGN");
-    p.walign = al_env ? (uint32_t)atoi(al_env) : 0u;  // 2: dense aligned chunks (copy_chunks)
-    // tile prefixes: every thread of the workgroup sums some predecessors' aggregates
-    // (lookback_partial; same box: C2 walk 0.2085-0.2086 vs 0.2091-0.2106 ms, C4 decode
-    // 0.0676-0.0679 vs 0.0686-0.0689 ms, profiles/r05t); LSMGPU_WSC_LOOKBACK=window keeps the
-    // windowed decoupled look-back
-    const char* lb_env = getenv("LSMGPU_WSC_LOOKBACK");
-    p.wlbfull = lb_env && strcmp(lb_env, "window") == 0 ? 0u : 1u;
-    // group walks (<= 64 blocks per CU, e.g. one 64 MiB table): 8 lanes per block forward plus 8
-    // walking backward from the terminator in other waves (kWalkGroupBi; same box, C4: walk
-    // 0.0402-0.0411 -> 0.0341-0.0354 ms, decode 0.0676-0.0688 -> 0.0614-0.0626 ms, profiles/r05z,
-    // r05aa; 16 + 16 lanes: 0.0378-0.0381).  LSMGPU_WSC_BIDIR=0 / 1 / 2: off / 8 + 8 / 16 + 16
-    const char* bi_env = getenv("LSMGPU_WSC_BIDIR");
-    p.wbidir = bi_env ? (uint32_t)std::min(std::max(atoi(bi_env), 0), 2) : 1u;
-    const char* pad_env = getenv("LSMGPU_WSC_PADLDS");  // experiments only: fewer tiles per CU
-    p.wpad = pad_env ? (uint32_t)atoi(pad_env) : 0u;
-    const char* ww_env = getenv("LSMGPU_WSC_WIDE");
     const uint64_t cus = (uint64_t)c->num_cus;
+    // The adopted configuration (DESIGN.md 5 has the measurements behind each choice):
+    // * copy: two waves per block above 8 KiB (C5 1.25 -> 1.09 ms);
+    // * view-only decodes finish inside the walk when there are >= 2 walk tiles (256 blocks) per
+    //   CU (C2 1 GiB 0.413 -> 0.323 ms; with fewer the tile epilogues run on too few workgroups,
+    //   C4 0.085 -> 0.165 ms);
+    // * lane walks: 576-block tiles (9 waves, 2 workgroups per CU) when 256-block ones (4 per CU,
+    //   LDS-bound) would not all be resident at once and 576-block ones would (C2 2^30 B: walk
+    //   0.2296 -> 0.210 ms), sized for two equal waves of tiles (walk 0.2099 -> 0.2062 ms), and for
+    //   materialize two tiles per workgroup walked back to back (walk 0.2059 -> 0.2011 ms);
+    // * <= 64 blocks per CU (e.g. one 64 MiB table): 8 lanes per block guessing same-shape runs
+    //   forward plus 8 walking backward from the terminator (C4 walk 0.0402 -> 0.0341 ms); else
+    //   one lane per block (C2 1 GiB: lane 0.733 vs group 0.799 ms).
+    // Test hooks (they choose among these compiled paths only): LSMGPU_WSC_VIEWFUSE=0|1,
+    // LSMGPU_WSC_WIDE=0|1, LSMGPU_WSC_WALK=lane|group.
+    p.wsplit = max_blk_len > 8192 ? 2u : 1u;
+    const char* vf_env = getenv("LSMGPU_WSC_VIEWFUSE");
+    const bool fuse = vf_env ? atoi(vf_env) != 0 : nblk >= 512ull * cus;
+    p.wfuse = !(mode & LSMGPU_MODE_MATERIALIZE) && fuse;
+    const char* ww_env = getenv("LSMGPU_WSC_WIDE");
     p.wwide = ww_env ? (atoi(ww_env) != 0 ? 576u : 0u)
                      : ((nblk + 255) / 256 > 4 * cus && (nblk + 575) / 576 <= 2 * cus ? 576u : 0u);
-    // wide tiles: just enough blocks for two equal waves of tiles at one workgroup per CU (C2
-    // 2^30 B: 521 blocks, 512 tiles; same box, walk 0.2099-0.2108 -> 0.2062-0.2089 ms, view
-    // 0.2314 -> 0.228-0.2283 ms, profiles/r05af), or LSMGPU_WSC_TBE=0: 576 blocks each
-    const char* tbe_env = getenv("LSMGPU_WSC_TBE");
     p.wtbe = 576u;
-    if (p.wwide && !(tbe_env && atoi(tbe_env) == 0))
-      p.wtbe = (uint32_t)std::min<uint64_t>(576, std::max<uint64_t>(64, (nblk + 2 * cus - 1) / (2 * cus)));
-    // wide materialize walks: two tiles per workgroup, walked back to back before their
-    // look-backs (wsc_walk_persist_kernel; same box, C2 2^30 B: walk 0.2059-0.2066 ->
-    // 0.2011-0.2013 ms, decode 1,422 -> 1,435-1,436 GiB/s, profiles/r05ar); LSMGPU_WSC_PERSIST=0
-    // keeps one tile per workgroup
-    const char* ps_env = getenv("LSMGPU_WSC_PERSIST");
-    p.wpersist = ps_env && atoi(ps_env) == 0 ? 0u : 1u;
-
+    if (p.wwide) p.wtbe = (uint32_t)std::min<uint64_t>(576, std::max<uint64_t>(64, (nblk + 2 * cus - 1) / (2 * cus)));
+    p.wwalk = nblk <= 64ull * cus ? kWalkGroup : kWalkLane;
     const char* wk_env = getenv("LSMGPU_WSC_WALK");
-    // Default: 8 lanes per block guessing same-shape runs (kWalkGroup) when the batch has at
-    // most 64 blocks per CU -- one lane per block would leave the machine idle and the walk is
-    // pure latency (C4 64 MiB, 5,163 blocks: 0.106 -> 0.071 ms) -- else one lane per block
-    // (C2 1 GiB: lane 0.733 vs group 0.799 ms; C5 1 GiB, 185 blocks per CU whose shapes
-    // rarely repeat: lane 1.02 vs group 1.08 ms with its give-up rule, 1.66 ms without).
-    // LSMGPU_WSC_WALK=lane / group / group2 / group4 / group16 / group32 / group64 (staged in LDS)
-    // forces a walk.
-    p.wwalk = nblk <= 64ull * (uint64_t)c->num_cus ? kWalkGroup : kWalkLane;
+    if (wk_env && wk_env[0] == 'l') p.wwalk = kWalkLane;
+    else if (wk_env && strncmp(wk_env, "group", 5) == 0) p.wwalk = kWalkGroup;
     p.wlanes = p.wwalk == kWalkGroup ? 8 : 1;
-    if (wk_env && wk_env[0] == 'l') {
-      p.wwalk = kWalkLane;
-      p.wlanes = 1;
-    } else if (wk_env && strncmp(wk_env, "group", 5) == 0) {
-      const int l = atoi(wk_env + 5);  // "group" alone: 8 lanes
-      p.wwalk = kWalkGroup;
-      p.wlanes = l == 2 || l == 4 || l == 16 || l == 32 || l == 64 ? (uint32_t)l : 8u;  // "group2" ... "group64"
-    }
-    // lane walks (materialize): LSMGPU_WSC_EO=1 has the walk's epilogue write the per-entry
-    // outputs instead of the copy (p.weo).  Off: same box, C2 copy 0.4992-0.5 -> 0.4547-0.4561 ms
-    // but walk 0.2088-0.209 -> 0.2556-0.2569 ms (the epilogue's record re-reads are a dependent
-    // chain per wave at 1 workgroup per CU), decode 1,402-1,404 -> 1,396-1,398 GiB/s (r05ac)
-    const char* es_env = getenv("LSMGPU_WSC_EOSEP");
-    p.weosep = es_env && atoi(es_env) == 1 ? 1u : 0u;
-    const char* eo_env = getenv("LSMGPU_WSC_EO");
-    p.weo = p.wwalk == kWalkLane && !p.wfuse && eo_env && atoi(eo_env) == 1 ? 1u : 0u;
-    // the 64-lane staged walk copies its own blocks from LDS (no copy launch, one read of the
-    // input) unless LSMGPU_WSC_STAGECOPY=0
-    const char* sc_env = getenv("LSMGPU_WSC_STAGECOPY");
-    p.wscopy = p.wwalk == kWalkGroup && p.wlanes == 64 && !p.wfuse && !(sc_env && atoi(sc_env) == 0);
-    // group walk: a new round after each odd-shaped entry; LSMGPU_WSC_SUB=1 re-guesses inside the
-    // round instead (sub-rounds: C4 walk 0.0407 vs 0.0384 ms, profiles/r04i -- not adopted)
-    const char* sub_env = getenv("LSMGPU_WSC_SUB");
-    p.wsub = sub_env && atoi(sub_env) == 1 ? 1u : 0u;
-    // group walk: the round's two lane exchanges through LDS shuffles; LSMGPU_WSC_DPP=1 uses
-    // DPP OR-reductions instead (C4 walk 0.0395 vs 0.0392-0.0397 ms, profiles/r04l: no gain)
-    const char* dpp_env = getenv("LSMGPU_WSC_DPP");
-    p.wdpp = dpp_env && atoi(dpp_env) == 1 ? 1u : 0u;
-    // view-only lane walk: each pass's entry owners by a scatter of block starts + a DPP max-scan
-    // (C2 view 0.2677 / 0.2671 -> 0.2595 / 0.2604 ms, profiles/r04l); LSMGPU_WSC_VIEWSCAN=0: the
-    // 6-step lane-shuffle binary search
-    const char* vs_env = getenv("LSMGPU_WSC_VIEWSCAN");
-    p.wview = vs_env && atoi(vs_env) == 0 ? 0u : 1u;
-    const char* sl_env = getenv("LSMGPU_WSC_SLOT");  // A/B: "small" LDS slots (4.25 KiB)
-    p.wslot = sl_env && sl_env[0] == 's' ? 1u : (sl_env && sl_env[0] == 'n' ? 2u : 0u);  // "none": global
+    // the diagnostic build's defaults of its extra knobs are the product's fixed choices
+    p.wchunk = 32u;
+    p.wkeep = 1u;
+    p.wtile = 256u;
+    p.wlbfull = 1u;
+    p.wbidir = 1u;
+    p.wpersist = 1u;
+    p.wview = 1u;
+#ifdef LSMGPU_DIAG
+    decode_diag_knobs(p, nblk, cus, max_blk_len, wk_env);
+#endif
     // d_result is zeroed by the walk kernel when a copy launch follows it (the copy's atomics
     // come after the kernel boundary): one operation fewer per decode.  A view-only decode
     // that ends in the walk updates d_result from every workgroup, so it is zeroed first.
@@ -589,7 +477,7 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
       HIPC(hipMemsetAsync(p.stamps, 0, 16 * sizeof(uint64_t), c->stream));  // walk counters
     }
 #endif
-    if (p.wfuse || p.wscopy) HIPC(hipMemsetAsync(d_result, 0, 8 * sizeof(uint64_t), c->stream));
+    if (p.wfuse || LSMGPU_KNOB(p.wscopy, 0u)) HIPC(hipMemsetAsync(d_result, 0, 8 * sizeof(uint64_t), c->stream));
     else p.zero_result = 1;
     if (c->ktime) HIPC(hipEventRecord(c->kev[0], c->stream));
     HIPC(launch_decode_wsc(p, c->stream, c->ktime ? c->kev[1] : nullptr));
@@ -605,98 +493,43 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
   return LSMGPU_OK;
 }
 
+// ABI 4: no page-locking (host_io.hpp); the registry keeps ABI 3's argument and error rules
 int lsmgpu_host_register(lsmgpu_ctx* c, void* p, uint64_t bytes) {
   if (!c || !p || !bytes || (uintptr_t)p + bytes < (uintptr_t)p) return LSMGPU_ERR_ARG;
   HIPC(hipSetDevice(c->device));
-  PinRegistry& R = pins();
-  std::unique_lock<std::shared_mutex> g(R.mu());
-  // pin only the pages no segment covers yet, each run as a segment of its own
-  const std::vector<PinRegistry::Range> gaps = R.gaps((uintptr_t)p, bytes);
-  // a gap the runtime already knows as page-locked memory was pinned outside the library
-  for (const auto& gp : gaps)
-    if (pinned_elsewhere(reinterpret_cast<void*>(std::max<uintptr_t>(gp.first, (uintptr_t)p))) ||
-        pinned_elsewhere(reinterpret_cast<void*>(std::min<uintptr_t>(gp.second, (uintptr_t)p + bytes) - 1)))
-      return LSMGPU_ERR_HOST_PINNED;
-  std::vector<PinRegistry::Range> made;
-  int rc = LSMGPU_OK;
-  for (const auto& gp : gaps) {
-    void* q = reinterpret_cast<void*>(gp.first);
-    const size_t n = gp.second - gp.first;
-    hipError_t e = hipHostRegister(q, n, hipHostRegisterPortable);
-    if (e != hipSuccess && e != hipErrorHostMemoryAlreadyRegistered) {
-      (void)hipGetLastError();  // a PROT_READ mapping (an mmap'd .sst) pins read-only
-      e = hipHostRegister(q, n, hipHostRegisterPortable | hipHostRegisterReadOnly);
-    }
-    if (e != hipSuccess) {
-      report_hip_error("hipHostRegister", e, __LINE__);
-      (void)hipGetLastError();
-      // pinned outside this library (hipHostMalloc, the caller's own hipHostRegister): those
-      // pages are not ours to pin or unpin, and nothing of the range is registered here
-      rc = e == hipErrorHostMemoryAlreadyRegistered ? LSMGPU_ERR_HOST_PINNED : LSMGPU_ERR_HIP;
-      break;
-    }
-    if (debug_pin())
-      fprintf(stderr, "lsmgpu: pin [%#lx, %#lx) for [%p, +%llu)\n", (unsigned long)gp.first,
-              (unsigned long)gp.second, p, (unsigned long long)bytes);
-    made.push_back(gp);
-  }
-  if (rc != LSMGPU_OK) {
-    for (const auto& m : made) (void)hipHostUnregister(reinterpret_cast<void*>(m.first));
-    (void)hipGetLastError();
-    return rc;
-  }
-  R.add((uintptr_t)p, bytes, made);
+  // page-locked outside this library (hipHostMalloc, lsmgpu_host_alloc, a caller's own
+  // hipHostRegister): it is DMA'd directly and needs no registration
+  const uint8_t* q = static_cast<const uint8_t*>(p);
+  if (runtime_pinned(q, 1) || runtime_pinned(q + bytes - 1, 1)) return LSMGPU_ERR_HOST_PINNED;
+  HostRanges& R = host_ranges();
+  std::lock_guard<std::mutex> g(R.mu);
+  R.r.emplace((uintptr_t)p, bytes);
   return LSMGPU_OK;
 }
 
 int lsmgpu_host_unregister(lsmgpu_ctx* c, void* p) {
   if (!c || !p) return LSMGPU_ERR_ARG;
+  HostRanges& R = host_ranges();
+  std::lock_guard<std::mutex> g(R.mu);
+  auto it = R.r.find((uintptr_t)p);
+  if (it == R.r.end()) return LSMGPU_ERR_ARG;  // not registered
+  R.r.erase(it);
+  return LSMGPU_OK;
+}
+
+int lsmgpu_host_alloc(lsmgpu_ctx* c, uint64_t bytes, void** out) {
+  if (!c || !out || !bytes) return LSMGPU_ERR_ARG;
+  *out = nullptr;
   HIPC(hipSetDevice(c->device));
-  PinRegistry& R = pins();
-  std::unique_lock<std::shared_mutex> g(R.mu());
-  std::vector<PinRegistry::Range> unpin, repin;
-  bool recut = false;
-  if (!R.remove((uintptr_t)p, &unpin, &repin, &recut)) return LSMGPU_ERR_ARG;  // not registered here
-  if (!unpin.empty()) {
-    // drain every device before unpinning: no copy from those pages may be in flight (a re-cut
-    // unpins pages other ranges still use; new copies wait on the lock), and the runtime releases
-    // a registration whose copies have all retired at once, not later -- a deferred release could
-    // otherwise unpin pages a later registration of the same addresses has pinned again
-    int ndev = 0;
-    (void)hipGetDeviceCount(&ndev);
-    for (int d = 0; d < ndev; d++)
-      if (hipSetDevice(d) == hipSuccess) (void)hipDeviceSynchronize();
-    (void)hipSetDevice(c->device);
-    (void)hipGetLastError();
-  }
-  (void)recut;
-  int rc = LSMGPU_OK;
-  for (const auto& r : unpin) {
-    if (debug_pin())
-      fprintf(stderr, "lsmgpu: unpin [%#lx, %#lx) (recut %d)\n", (unsigned long)r.first,
-              (unsigned long)r.second, (int)recut);
-    hipError_t e = hipHostUnregister(reinterpret_cast<void*>(r.first));
-    if (e != hipSuccess) {
-      report_hip_error("hipHostUnregister", e, __LINE__);
-      (void)hipGetLastError();
-      rc = LSMGPU_ERR_HIP;
-    }
-  }
-  for (const auto& r : repin) {
-    void* q = reinterpret_cast<void*>(r.first);
-    hipError_t e = hipHostRegister(q, r.second - r.first, hipHostRegisterPortable);
-    if (e != hipSuccess) {
-      (void)hipGetLastError();
-      e = hipHostRegister(q, r.second - r.first, hipHostRegisterPortable | hipHostRegisterReadOnly);
-    }
-    if (e != hipSuccess) {  // those pages stay unpinned: copies from them are staged, still correct
-      report_hip_error("hipHostRegister (re-cut)", e, __LINE__);
-      (void)hipGetLastError();
-      R.drop(r);
-      rc = LSMGPU_ERR_HIP;
-    }
-  }
-  return rc;
+  HIPC(hipHostMalloc(out, bytes, hipHostMallocPortable));
+  return LSMGPU_OK;
+}
+
+int lsmgpu_host_free(lsmgpu_ctx* c, void* p) {
+  if (!p) return LSMGPU_OK;
+  if (c) HIPC(hipSetDevice(c->device));
+  HIPC(hipHostFree(p));
+  return LSMGPU_OK;
 }
 
 }  // extern "C"
@@ -718,6 +551,16 @@ __global__ void __launch_bounds__(256) add_bases_kernel(uint32_t* ke, uint32_t* 
 
 constexpr int kNotPipelined = -1;
 
+// A pipeline slot's staged outputs into the caller's arrays, once their D2H has landed
+hipError_t drain(lsmgpu_ctx* c, lsmgpu_ctx::Slot& sl) {
+  if (sl.drains.empty()) return hipSuccess;
+  const hipError_t e = hipEventSynchronize(sl.out_done);
+  if (e != hipSuccess) return e;
+  for (const auto& d : sl.drains) c->pool->copy(d.dst, sl.pin_out.p + d.at, d.n);
+  sl.drains.clear();
+  return hipSuccess;
+}
+
 // lsmgpu_decode_blocks for host memory, as a pipeline: the blocks (sorted by offset, disjoint)
 // are cut into chunks of ~64 MiB of input; chunk c's copy-in (s_in), decode (ctx stream) and
 // copy-out (s_out) overlap chunk c+1's copy-in and chunk c-1's copy-out, over kSlots device
@@ -730,7 +573,7 @@ int decode_host_pipelined(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
                           const uint32_t* blk_off, const uint32_t* blk_len, uint64_t nblk,
                           int mode, lsmgpu_decoded* out, uint32_t max_len) {
   const char* ch_env = getenv("LSMGPU_HOST_CHUNK");
-  const uint64_t chunk = ch_env && atoll(ch_env) >= (1 << 20) ? (uint64_t)atoll(ch_env) : (64ull << 20);
+  const uint64_t chunk = ch_env && atoll(ch_env) >= (1 << 20) ? (uint64_t)atoll(ch_env) : (32ull << 20);
   if (max_len >= 65536 || nblk < 2) return kNotPipelined;
   for (uint64_t b = 0; b < nblk; b++) {
     if ((uint64_t)blk_off[b] + blk_len[b] > data_len) return kNotPipelined;
@@ -750,6 +593,10 @@ int decode_host_pipelined(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
   }
   const bool mat = (mode & LSMGPU_MODE_MATERIALIZE) != 0, view = (mode & LSMGPU_MODE_VIEW) != 0;
   const uint64_t ecap = max_span / 10 + 1;  // >= 10 B per entry (its header)
+  // input: DMA'd straight from runtime-pinned memory (lsmgpu_host_alloc), else memcpy'd into the
+  // slot's pin_in first; the chunk's block offsets / lengths always go through pin_in
+  const bool in_direct = runtime_pinned(data, data_len);
+  const uint64_t idx_at_max = in_direct ? 0 : (max_span + 255) / 256 * 256;
   if (!c->s_in) HIPC(hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking));
   if (!c->s_out) HIPC(hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking));
   if (!c->h_chunk_res)
@@ -771,6 +618,10 @@ int decode_host_pipelined(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
     if (view) HIPC(sl.view.ensure(ecap * 8));
     for (hipEvent_t* e : {&sl.in_done, &sl.dec_done, &sl.out_done})
       if (!*e) HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    // (no DMA of an earlier call is in flight: every call drains its streams before returning)
+    HIPC(sl.pin_in.ensure(idx_at_max + max_nb * 8 + 256));
+    sl.drains.clear();
+    sl.in_used = false;
   }
   // every return below (errors included) first drains the three streams: no copy into the
   // caller's arrays outlives the call
@@ -788,12 +639,23 @@ int decode_host_pipelined(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
       auto& sl = c->slot[i % lsmgpu_ctx::kSlots];
       const uint64_t b0 = cb[i], nb = cb[i + 1] - b0;
       const uint64_t a = blk_off[b0] & ~127ull, e = (uint64_t)blk_off[cb[i + 1] - 1] + blk_len[cb[i + 1] - 1];
+      if (sl.in_used) HIPC(hipEventSynchronize(sl.in_done));  // pin_in's last DMA is done
+      const uint64_t idx_at = in_direct ? 0 : (e - a + 255) / 256 * 256;
+      const uint8_t* src = data + a;
+      if (!in_direct) {
+        c->pool->copy(sl.pin_in.p, data + a, e - a);
+        src = sl.pin_in.p;
+      }
+      std::memcpy(sl.pin_in.p + idx_at, blk_off + b0, nb * 4);
+      std::memcpy(sl.pin_in.p + idx_at + nb * 4, blk_len + b0, nb * 4);
       if (slot_used[i % lsmgpu_ctx::kSlots]) HIPC(hipStreamWaitEvent(c->s_in, sl.out_done, 0));
       slot_used[i % lsmgpu_ctx::kSlots] = 1;
-      HIPC(hcopy(sl.data.p, data + a, e - a, hipMemcpyHostToDevice, c->s_in));
-      HIPC(hcopy(sl.off.p, blk_off + b0, nb * 4, hipMemcpyHostToDevice, c->s_in));
-      HIPC(hcopy(sl.len.p, blk_len + b0, nb * 4, hipMemcpyHostToDevice, c->s_in));
+      HIPC(hipMemcpyAsync(sl.data.p, src, e - a, hipMemcpyHostToDevice, c->s_in));
+      HIPC(hipMemcpyAsync(sl.off.p, sl.pin_in.p + idx_at, nb * 4, hipMemcpyHostToDevice, c->s_in));
+      HIPC(hipMemcpyAsync(sl.len.p, sl.pin_in.p + idx_at + nb * 4, nb * 4, hipMemcpyHostToDevice,
+                          c->s_in));
       HIPC(hipEventRecord(sl.in_done, c->s_in));
+      sl.in_used = true;
       HIPC(hipStreamWaitEvent(c->stream, sl.in_done, 0));
       lsmgpu_decoded d{};
       if (mat) {
@@ -845,26 +707,53 @@ int decode_host_pipelined(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
                          out->blk_first ? nb1 : 0u, (uint32_t)E);
       HIPC(hipGetLastError());
     }
-    auto back = [&](void* hp, const void* dp, uint64_t bytes) -> hipError_t {
-      if (!hp || !bytes) return hipSuccess;
-      return hcopy(hp, dp, bytes, hipMemcpyDeviceToHost, c->s_out);
+    // outputs: straight into runtime-pinned caller arrays, else into the slot's pin_out, drained
+    // into the caller's arrays by the host while the next chunk's copies run
+    struct Piece {
+      void* hp;
+      const void* dp;
+      uint64_t n;
+    } pcs[7];
+    int np = 0;
+    auto add = [&](void* hp, const void* dp, uint64_t bytes) {
+      if (hp && bytes) pcs[np++] = {hp, dp, bytes};
     };
     if (fits) {
       if (mat) {
-        HIPC(back(out->key_data ? out->key_data + KB : nullptr, sl.kd.p, kb));
-        HIPC(back(out->val_data ? out->val_data + VB : nullptr, sl.vd.p, vb));
-        HIPC(back(out->key_end ? out->key_end + E : nullptr, sl.ke.p, n * 4));
-        HIPC(back(out->val_end ? out->val_end + E : nullptr, sl.ve.p, n * 4));
+        add(out->key_data ? out->key_data + KB : nullptr, sl.kd.p, kb);
+        add(out->val_data ? out->val_data + VB : nullptr, sl.vd.p, vb);
+        add(out->key_end ? out->key_end + E : nullptr, sl.ke.p, n * 4);
+        add(out->val_end ? out->val_end + E : nullptr, sl.ve.p, n * 4);
       }
-      if (view) HIPC(back(out->view ? out->view + E : nullptr, sl.view.p, n * 8));
+      if (view) add(out->view ? out->view + E : nullptr, sl.view.p, n * 8);
     }
-    HIPC(back(out->blk_first ? out->blk_first + b0 : nullptr, sl.bf.p, (nb + (last ? 1 : 0)) * 4));
-    HIPC(back(out->blk_status ? out->blk_status + b0 : nullptr, sl.bs.p, nb * 4));
+    add(out->blk_first ? out->blk_first + b0 : nullptr, sl.bf.p, (nb + (last ? 1 : 0)) * 4);
+    add(out->blk_status ? out->blk_status + b0 : nullptr, sl.bs.p, nb * 4);
+    bool direct[7];
+    uint64_t need = 0;
+    for (int k = 0; k < np; k++) {
+      direct[k] = runtime_pinned(pcs[k].hp, pcs[k].n);
+      if (!direct[k]) need += (pcs[k].n + 15) / 16 * 16;
+    }
+    // (slot j's previous chunk, j - kSlots, was drained while chunk j - 1 was placed)
+    HIPC(sl.pin_out.ensure(need));
+    uint64_t at = 0;
+    for (int k = 0; k < np; k++) {
+      if (direct[k]) {
+        HIPC(hipMemcpyAsync(pcs[k].hp, pcs[k].dp, pcs[k].n, hipMemcpyDeviceToHost, c->s_out));
+      } else {
+        HIPC(hipMemcpyAsync(sl.pin_out.p + at, pcs[k].dp, pcs[k].n, hipMemcpyDeviceToHost, c->s_out));
+        sl.drains.push_back({pcs[k].hp, at, pcs[k].n});
+        at += (pcs[k].n + 15) / 16 * 16;
+      }
+    }
     HIPC(hipEventRecord(sl.out_done, c->s_out));
+    if (j) HIPC(drain(c, c->slot[(j - 1) % lsmgpu_ctx::kSlots]));
     E += n;
     KB += kb;
     VB += vb;
   }
+  HIPC(drain(c, c->slot[(nch - 1) % lsmgpu_ctx::kSlots]));
   HIPC(hipStreamSynchronize(c->s_out));
   out->n_entries = E;
   out->key_bytes = KB;
@@ -886,7 +775,6 @@ int lsmgpu_decode_blocks(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
   if (data_len > 0xffffffffull) return LSMGPU_ERR_TOO_LARGE;
   if (mode & ~(LSMGPU_MODE_MATERIALIZE | LSMGPU_MODE_VIEW)) return LSMGPU_ERR_ARG;
   HIPC(hipSetDevice(c->device));
-  if (!data_on_device) (void)bounce_buf();  // (before any copy can be refused)
   uint32_t max_len = 0;
   for (uint64_t b = 0; b < nblk; b++) max_len = std::max(max_len, blk_len[b]);
   const bool query0 = !out->key_data && !out->key_end && !out->val_data && !out->val_end &&
@@ -900,8 +788,8 @@ int lsmgpu_decode_blocks(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
   HIPC(c->s_off.ensure((nblk + 1) * 4));
   HIPC(c->s_len.ensure((nblk + 1) * 4));
   if (nblk) {
-    HIPC(hcopy(c->s_off.p, blk_off, nblk * 4, hipMemcpyHostToDevice, c->stream));
-    HIPC(hcopy(c->s_len.p, blk_len, nblk * 4, hipMemcpyHostToDevice, c->stream));
+    HIPC(hcopy(c, c->s_off.p, blk_off, nblk * 4, hipMemcpyHostToDevice, c->stream));
+    HIPC(hcopy(c, c->s_len.p, blk_len, nblk * 4, hipMemcpyHostToDevice, c->stream));
   }
   lsmgpu_decoded d = *out;
   // every output pointer NULL = a size query: the blocks are walked, n_entries / key_bytes /
@@ -915,7 +803,7 @@ int lsmgpu_decode_blocks(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
   const uint8_t* d_data = data;
   if (!data_on_device) {  // stage host buffers through HBM
     HIPC(c->s_data.ensure(data_len + 16));
-    if (data_len) HIPC(hcopy(c->s_data.p, data, data_len, hipMemcpyHostToDevice, c->stream));
+    if (data_len) HIPC(hcopy(c, c->s_data.p, data, data_len, hipMemcpyHostToDevice, c->stream));
     d_data = c->s_data.as<uint8_t>();
     auto stage = [&](DevBuf& b, void* hp, uint64_t bytes) -> void* {
       if (!hp) return nullptr;
@@ -949,7 +837,7 @@ int lsmgpu_decode_blocks(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
   if (!data_on_device) {
     auto back = [&](void* hp, const void* dp, uint64_t bytes) -> hipError_t {
       if (!hp || !bytes) return hipSuccess;
-      return hcopy(hp, dp, bytes, hipMemcpyDeviceToHost, c->stream);
+      return hcopy(c, hp, dp, bytes, hipMemcpyDeviceToHost, c->stream);
     };
     const bool fits = !(flags & 1);
     uint64_t ne = fits ? out->n_entries : 0;
@@ -1049,7 +937,6 @@ int lsmgpu_encode_blocks(lsmgpu_ctx* c, const uint8_t* keys, const uint32_t* key
   if (query && on_device && !c) return LSMGPU_ERR_ARG;
   if (epb == 0 && block_bytes == 0) return LSMGPU_ERR_ARG;
   if (c) HIPC(hipSetDevice(c->device));
-  if (c && !on_device) (void)bounce_buf();  // (before any copy can be refused)
   SyncOnExit sync_exit;
   if (c) sync_exit.s[0] = c->stream;
   // host copies of the offset columns (needed for totals and the byte-target plan)
@@ -1059,8 +946,8 @@ int lsmgpu_encode_blocks(lsmgpu_ctx* c, const uint8_t* keys, const uint32_t* key
   if (on_device && n) {
     hk.resize(n);
     hv.resize(n);
-    HIPC(hcopy(hk.data(), key_end, n * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPC(hcopy(hv.data(), vs_end, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hcopy(c, hk.data(), key_end, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hcopy(c, hv.data(), vs_end, n * 4, hipMemcpyDeviceToHost, c->stream));
     HIPC(hipStreamSynchronize(c->stream));
     hke = hk.data();
     hve = hv.data();
@@ -1103,11 +990,11 @@ int lsmgpu_encode_blocks(lsmgpu_ctx* c, const uint8_t* keys, const uint32_t* key
     HIPC(c->s_c.ensure(vs_total + 16));
     HIPC(c->s_d.ensure(n * 4 + 16));
     HIPC(c->s_kd.ensure(total + 16));
-    if (key_total) HIPC(hcopy(c->s_a.p, keys, key_total, hipMemcpyHostToDevice, c->stream));
-    if (vs_total) HIPC(hcopy(c->s_c.p, vs, vs_total, hipMemcpyHostToDevice, c->stream));
+    if (key_total) HIPC(hcopy(c, c->s_a.p, keys, key_total, hipMemcpyHostToDevice, c->stream));
+    if (vs_total) HIPC(hcopy(c, c->s_c.p, vs, vs_total, hipMemcpyHostToDevice, c->stream));
     if (n) {
-      HIPC(hcopy(c->s_b.p, key_end, n * 4, hipMemcpyHostToDevice, c->stream));
-      HIPC(hcopy(c->s_d.p, vs_end, n * 4, hipMemcpyHostToDevice, c->stream));
+      HIPC(hcopy(c, c->s_b.p, key_end, n * 4, hipMemcpyHostToDevice, c->stream));
+      HIPC(hcopy(c, c->s_d.p, vs_end, n * 4, hipMemcpyHostToDevice, c->stream));
     }
     dk = c->s_a.as<uint8_t>();
     dke = c->s_b.as<uint32_t>();
@@ -1118,7 +1005,7 @@ int lsmgpu_encode_blocks(lsmgpu_ctx* c, const uint8_t* keys, const uint32_t* key
   const uint32_t* dplan = nullptr;
   if (explicit_plan) {
     HIPC(c->s_bf.ensure((nb + 1) * 4));
-    HIPC(hcopy(c->s_bf.p, plan.data(), (nb + 1) * 4, hipMemcpyHostToDevice, c->stream));
+    HIPC(hcopy(c, c->s_bf.p, plan.data(), (nb + 1) * 4, hipMemcpyHostToDevice, c->stream));
     dplan = c->s_bf.as<uint32_t>();
   }
   HIPC(hipMemsetAsync(c->flags.p, 0, 16, c->stream));
@@ -1126,8 +1013,8 @@ int lsmgpu_encode_blocks(lsmgpu_ctx* c, const uint8_t* keys, const uint32_t* key
                                       dout, total, c->flags.as<uint32_t>());
   if (rc != LSMGPU_OK) return rc;
   uint32_t hflags[4] = {0, 0, 0, 0};
-  HIPC(hcopy(hflags, c->flags.p, 16, hipMemcpyDeviceToHost, c->stream));
-  if (!on_device) HIPC(hcopy(out, dout, total, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hcopy(c, hflags, c->flags.p, 16, hipMemcpyDeviceToHost, c->stream));
+  if (!on_device) HIPC(hcopy(c, out, dout, total, hipMemcpyDeviceToHost, c->stream));
   HIPC(hipStreamSynchronize(c->stream));
   if (hflags[0] & 1) return LSMGPU_ERR_KEY_LEN;
   if (hflags[0] & 2) return LSMGPU_ERR_VALUE_LEN;
@@ -1135,7 +1022,7 @@ int lsmgpu_encode_blocks(lsmgpu_ctx* c, const uint8_t* keys, const uint32_t* key
     if (nb > restarts_cap) return LSMGPU_ERR_CAPACITY;
     std::vector<uint8_t> idx(4 * nb);
     if (on_device) {
-      HIPC(hcopy(idx.data(), out + dl, 4 * nb, hipMemcpyDeviceToHost, c->stream));
+      HIPC(hcopy(c, idx.data(), out + dl, 4 * nb, hipMemcpyDeviceToHost, c->stream));
       HIPC(hipStreamSynchronize(c->stream));
     } else {
       std::memcpy(idx.data(), out + dl, 4 * nb);
@@ -1160,7 +1047,7 @@ int lsmgpu_encode_values(lsmgpu_ctx* c, const uint8_t* meta, const uint8_t* user
   uint64_t vtotal = 0;
   if (on_device) {
     uint32_t last = 0;
-    HIPC(hcopy(&last, value_end + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hcopy(c, &last, value_end + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
     HIPC(hipStreamSynchronize(c->stream));
     vtotal = last;
   } else {
@@ -1179,11 +1066,11 @@ int lsmgpu_encode_values(lsmgpu_ctx* c, const uint8_t* meta, const uint8_t* user
     HIPC(c->s_d.ensure(n * 4 + 16));
     HIPC(c->s_ve.ensure(n * 4 + 16));
     uint8_t* dm = c->s_a.as<uint8_t>();
-    HIPC(hcopy(dm, meta, n, hipMemcpyHostToDevice, c->stream));
-    HIPC(hcopy(dm + n, user_meta, n, hipMemcpyHostToDevice, c->stream));
-    HIPC(hcopy(c->s_b.p, expires_at, n * 8, hipMemcpyHostToDevice, c->stream));
-    if (vtotal) HIPC(hcopy(c->s_c.p, values, vtotal, hipMemcpyHostToDevice, c->stream));
-    HIPC(hcopy(c->s_d.p, value_end, n * 4, hipMemcpyHostToDevice, c->stream));
+    HIPC(hcopy(c, dm, meta, n, hipMemcpyHostToDevice, c->stream));
+    HIPC(hcopy(c, dm + n, user_meta, n, hipMemcpyHostToDevice, c->stream));
+    HIPC(hcopy(c, c->s_b.p, expires_at, n * 8, hipMemcpyHostToDevice, c->stream));
+    if (vtotal) HIPC(hcopy(c, c->s_c.p, values, vtotal, hipMemcpyHostToDevice, c->stream));
+    HIPC(hcopy(c, c->s_d.p, value_end, n * 4, hipMemcpyHostToDevice, c->stream));
     p.meta = dm; p.user_meta = dm + n; p.expires_at = c->s_b.as<uint64_t>();
     p.values = c->s_c.as<uint8_t>(); p.value_end = c->s_d.as<uint32_t>();
     p.vs_end = c->s_ve.as<uint32_t>();
@@ -1201,7 +1088,7 @@ int lsmgpu_encode_values(lsmgpu_ctx* c, const uint8_t* meta, const uint8_t* user
                                rocprim::plus<uint32_t>(), c->stream));
   p.vs_end = final_end;
   uint32_t total = 0;
-  HIPC(hcopy(&total, p.vs_end + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hcopy(c, &total, p.vs_end + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
   HIPC(hipStreamSynchronize(c->stream));
   *vs_len = total;
   if (total > vs_cap) return LSMGPU_ERR_CAPACITY;
@@ -1211,8 +1098,8 @@ int lsmgpu_encode_values(lsmgpu_ctx* c, const uint8_t* meta, const uint8_t* user
   }
   HIPC(launch_values_write(p, c->stream));
   if (!on_device) {
-    HIPC(hcopy(vs, p.vs, total, hipMemcpyDeviceToHost, c->stream));
-    HIPC(hcopy(vs_end, p.vs_end, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hcopy(c, vs, p.vs, total, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hcopy(c, vs_end, p.vs_end, n * 4, hipMemcpyDeviceToHost, c->stream));
   }
   HIPC(hipStreamSynchronize(c->stream));
   return LSMGPU_OK;
@@ -1683,7 +1570,7 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
   HIPC(c->cp_data.ensure(data_len + 64));
   for (uint32_t t = 0; t < ntables; t++)
     if (base[t + 1] > base[t])
-      HIPC(hcopy(c->cp_data.as<uint8_t>() + base[t], ssts[t], base[t + 1] - base[t],
+      HIPC(hcopy(c, c->cp_data.as<uint8_t>() + base[t], ssts[t], base[t + 1] - base[t],
                           hipMemcpyHostToDevice, c->stream));
   HIPC(c->cp_res.ensure(64));
   uint64_t* d_res = c->cp_res.as<uint64_t>();
@@ -1695,8 +1582,8 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
     HIPC(c->cp_off.ensure(nb * 4 + 4));
     HIPC(c->cp_len.ensure(nb * 4 + 4));
     if (nb) {
-      HIPC(hcopy(c->cp_off.p, o.data(), nb * 4, hipMemcpyHostToDevice, c->stream));
-      HIPC(hcopy(c->cp_len.p, l.data(), nb * 4, hipMemcpyHostToDevice, c->stream));
+      HIPC(hcopy(c, c->cp_off.p, o.data(), nb * 4, hipMemcpyHostToDevice, c->stream));
+      HIPC(hcopy(c, c->cp_len.p, l.data(), nb * 4, hipMemcpyHostToDevice, c->stream));
     }
     uint64_t kcap = std::max<uint64_t>(data_len, 16), vcap = kcap, ecap = data_len / 10 + 1;
     for (int attempt = 0;; attempt++) {  // plen > 0 blocks can expand keys: resize once
@@ -1720,7 +1607,7 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
                                           c->cp_off.as<uint32_t>(), c->cp_len.as<uint32_t>(), nb,
                                           max_len, LSMGPU_MODE_MATERIALIZE, &d, d_res);
       if (rc != LSMGPU_OK) return rc;
-      HIPC(hcopy(r, d_res, 64, hipMemcpyDeviceToHost, c->stream));
+      HIPC(hcopy(c, r, d_res, 64, hipMemcpyDeviceToHost, c->stream));
       HIPC(hipStreamSynchronize(c->stream));
       if (r[5] & 2) return LSMGPU_ERR_INTERNAL;
       if (!(r[5] & 1)) break;
@@ -1731,8 +1618,8 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
     }
     bf.assign(nb + 1, 0);
     bs.assign(nb + 1, 0);
-    HIPC(hcopy(bf.data(), c->cp_bf.p, (nb + 1) * 4, hipMemcpyDeviceToHost, c->stream));
-    if (nb) HIPC(hcopy(bs.data(), c->cp_bs.p, nb * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hcopy(c, bf.data(), c->cp_bf.p, (nb + 1) * 4, hipMemcpyDeviceToHost, c->stream));
+    if (nb) HIPC(hcopy(c, bs.data(), c->cp_bs.p, nb * 4, hipMemcpyDeviceToHost, c->stream));
     HIPC(hipStreamSynchronize(c->stream));
     return LSMGPU_OK;
   };
@@ -1809,7 +1696,7 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
     return LSMGPU_OK;
   }
   HIPC(c->cp_rf.ensure((nruns + 1) * 4));
-  HIPC(hcopy(c->cp_rf.p, rf.data(), (nruns + 1) * 4, hipMemcpyHostToDevice, c->stream));
+  HIPC(hcopy(c, c->cp_rf.p, rf.data(), (nruns + 1) * 4, hipMemcpyHostToDevice, c->stream));
   // 4. MergeIterator (y/iterator.go:74-202): lower run index wins ties, duplicates dropped
   // the merge writes the merged order (source index + end offsets), not the bytes: the
   // encoder reads each entry's bytes from the decoded tables, the one copy builder.Add makes
@@ -1823,7 +1710,7 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
   int rc = lsmgpu_merge_runs_async(c, &runs, &mo, d_res);
   if (rc != LSMGPU_OK) return rc;
   uint64_t m[8];
-  HIPC(hcopy(m, d_res, 64, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hcopy(c, m, d_res, 64, hipMemcpyDeviceToHost, c->stream));
   HIPC(hipStreamSynchronize(c->stream));
   if (m[3] & LSMGPU_MERGE_TIMEOUT) return LSMGPU_ERR_INTERNAL;
   if (m[3] & LSMGPU_MERGE_KEY_LEN) return LSMGPU_ERR_KEY_LEN;
@@ -1843,7 +1730,7 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
                                     c->cp_tf.as<uint32_t>(), c->cp_tb.as<uint32_t>(),
                                     c->cp_to.as<uint64_t>(), (uint32_t)tcap, d_res);
     if (rc != LSMGPU_OK) return rc;
-    HIPC(hcopy(cut, d_res, 64, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hcopy(c, cut, d_res, 64, hipMemcpyDeviceToHost, c->stream));
     HIPC(hipStreamSynchronize(c->stream));
     if (!cut[3]) break;
     if (attempt || tcap >= mn) return LSMGPU_ERR_INTERNAL;
@@ -1866,8 +1753,8 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
   if (rc != LSMGPU_OK) return rc;
   std::vector<uint32_t> tf(nt + 1);
   c->cp_tbl_out.assign(nt + 1, 0);
-  HIPC(hcopy(tf.data(), c->cp_tf.p, (nt + 1) * 4, hipMemcpyDeviceToHost, c->stream));
-  HIPC(hcopy(c->cp_tbl_out.data(), c->cp_to.p, (nt + 1) * 8, hipMemcpyDeviceToHost,
+  HIPC(hcopy(c, tf.data(), c->cp_tf.p, (nt + 1) * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hcopy(c, c->cp_tbl_out.data(), c->cp_to.p, (nt + 1) * 8, hipMemcpyDeviceToHost,
                       c->stream));
   HIPC(hipStreamSynchronize(c->stream));
   if (bloom) {
@@ -1891,7 +1778,7 @@ extern "C" int lsmgpu_compact_tables(lsmgpu_ctx* c, const uint8_t* const* ssts,
     if (rc != LSMGPU_OK) return compact_fail(c, rc);
   }
   uint32_t fl[4];
-  HIPC(hcopy(fl, c->cp_flags.p, 16, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hcopy(c, fl, c->cp_flags.p, 16, hipMemcpyDeviceToHost, c->stream));
   HIPC(hipStreamSynchronize(c->stream));
   if ((fl[0] & 1) || (fl[1] & 1)) return LSMGPU_ERR_KEY_LEN;
   if (fl[0] & 2) return LSMGPU_ERR_VALUE_LEN;
@@ -1912,7 +1799,7 @@ extern "C" int lsmgpu_compact_result(lsmgpu_ctx* c, uint8_t* out, uint64_t out_c
   SyncOnExit sync_exit;
   sync_exit.s[0] = c->stream;
   if (c->cp_bytes)
-    HIPC(hcopy(out, c->cp_out.p, c->cp_bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hcopy(c, out, c->cp_out.p, c->cp_bytes, hipMemcpyDeviceToHost, c->stream));
   HIPC(hipStreamSynchronize(c->stream));
   std::memcpy(tbl_off, c->cp_tbl_out.data(), (nt + 1) * 8);
   return LSMGPU_OK;

@@ -382,7 +382,7 @@ __device__ __forceinline__ Plan walk_stage(const DecodeParams& p, const BlockRef
     pl.status = LSMGPU_BLK_RANGE;
     return pl;
   }
-  if (p.ablate & 4) return pl;
+  if ABLATE(p, 4) return pl;
   if (ref.fits) {
     if (ref.tail) land_tail(p, ref, slot, lane);
     wave_lds_fence();
@@ -443,7 +443,7 @@ __device__ __forceinline__ void emit_block(const DecodeParams& p, const Plan& pl
     ok = ok && kend < 0xffffffffull && vend <= 0xffffffffull;
   }
   if (!ok && lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(p.result + 5), 1ull);
-  if (!ok || pl.kind == 0 || (p.ablate & 2)) return;
+  if (!ok || pl.kind == 0 || ABLATE(p, 2)) return;
   if (pl.kind == 2) {
     emit_slow(p, p.data + pl.off, pl.n, ex.n, ex.k, ex.v, pl.off, lane);
     return;
@@ -592,7 +592,7 @@ __global__ void __launch_bounds__(64) decode_kernel(DecodeParams p) {
     if (k >= L) {
       const uint32_t ke = k - L, be = blk_of(ke);
       Tot ex{0, 0, 0};
-      if (!(p.ablate & 1)) ex = prefix_of(p, be, poll, tag, lane);
+      if (!ABLATE(p, 1)) ex = prefix_of(p, be, poll, tag, lane);
       mark(5);
       const uint32_t* rec = meta_of(ke);
       const Plan pl = plan_load(rec + MAXE + 2);
@@ -612,7 +612,7 @@ __global__ void __launch_bounds__(64) decode_kernel(DecodeParams p) {
       ref_next = prefetch_block<SLOT, Cfg::kIters>(p, readlane(ring_off, i), readlane(ring_len, i),
                                                    slot_of(k + 1), lane);
     }
-    if (k + 1 >= L && k + 1 - L < K && lane < 3 && !(p.ablate & 1))
+    if (k + 1 >= L && k + 1 - L < K && lane < 3 && !ABLATE(p, 1))
       poll = gload(p.lb + (uint64_t)blk_of(k + 1 - L) * 8 + 4 + lane);
     mark(2);
     // d. walk block k
@@ -623,7 +623,7 @@ __global__ void __launch_bounds__(64) decode_kernel(DecodeParams p) {
       const Plan pl = walk_stage<SLOT, MAXE>(p, ref, true, slot_of(k), rec, lane, spec_acc);
       plan_store(rec + MAXE + 2, pl, lane);
       mark(3);
-      if (!(p.ablate & 1)) {
+      if (!ABLATE(p, 1)) {
         store3(p.lb + (uint64_t)b * 8, tag, pl.n, pl.K, pl.V, lane);
         const uint32_t g0 = b & ~63u;
         const uint32_t gsize = (nblk - g0 < 64u) ? (nblk - g0) : 64u;
@@ -891,12 +891,12 @@ __device__ __forceinline__ void stage_block(const DecodeParams& p, const BlockRe
   const uint32_t kr = pl.ku >> 4;  // 16-B pieces per key
   const bool kdirect = pl.ku && (pl.ku & 15) == 0 && (kr & (kr - 1)) == 0;
   const uint32_t vbase = kdirect ? 0u : 16 * Qk;  // value stream's 16-aligned staging offset
-  if (!(p.ablate & 8)) {  // (timing-only ablation: 8 = no stream assembly)
+  if (!ABLATE(p, 8)) {  // (timing-only ablation: 8 = no stream assembly)
     if (!kdirect) assemble_stream<true>(stage, win, wsh, meta, pl.n, pl.K, pl.jk, pl.big, lane);
     assemble_stream<false>(stage + vbase, win, wsh, meta, pl.n, pl.V, pl.jv, pl.big, lane);
   }
   sub(3);
-  if (p.ablate & 16) return;  // (timing-only ablation: 16 = no register readback)
+  if ABLATE(p, 16) return;  // (timing-only ablation: 16 = no register readback)
   wave_lds_fence();
   const uint32_t ksh = kdirect ? __builtin_ctz(kr) : 0u;
   // chunk addresses (window coordinates): key chunks straight from the block (kdirect) or
@@ -968,7 +968,7 @@ __device__ __forceinline__ void emit_pend(const DecodeParams& p, const Pend& pd,
   if (p.stamps && lane == 0)  // blocks per emit path: [13] chunk mode, [14] piece mode, [15] global
     atomicAdd(reinterpret_cast<unsigned long long*>(p.stamps + (kind == 2 ? 15 : 13 + mode)), 1ull);
 #endif
-  if (!ok || kind == 0 || (p.ablate & 2)) return;
+  if (!ok || kind == 0 || ABLATE(p, 2)) return;
   if (kind == 2) {
     emit_slow(p, p.data + off, n, ex.n, ex.k, ex.v, off, lane);
     return;
@@ -1085,7 +1085,7 @@ __global__ void __launch_bounds__(64, 3) decode_reg_kernel(DecodeParams p) {  //
     if (k >= L) {
       const uint32_t be = blk_of(k - L);
       Tot ex{0, 0, 0};
-      if (!(p.ablate & 1)) ex = prefix_of(p, be, poll, tag, lane);
+      if (!ABLATE(p, 1)) ex = prefix_of(p, be, poll, tag, lane);
       mark(5);
       if (be == nblk - 1 && lane == 0) {  // totals of the whole batch
         const uint32_t n = readlane(pa.sc, 0), K = readlane(pa.sc, 1), V = readlane(pa.sc, 2);
@@ -1100,7 +1100,7 @@ __global__ void __launch_bounds__(64, 3) decode_reg_kernel(DecodeParams p) {  //
     pb = pc;
     mark(1);
     // c. next prefix poll, next block's bytes
-    if (k + 1 >= L && k + 1 - L < KW && lane < 3 && !(p.ablate & 1))
+    if (k + 1 >= L && k + 1 - L < KW && lane < 3 && !ABLATE(p, 1))
       poll = gload(p.lb + (uint64_t)blk_of(k + 1 - L) * 8 + 4 + lane);
     if (k + 1 < KW) {
       if (k + 1 - ring_k0 >= (uint32_t)kWave) ring_load(k + 1);
@@ -1115,13 +1115,13 @@ __global__ void __launch_bounds__(64, 3) decode_reg_kernel(DecodeParams p) {  //
       wave_lds_fence();
       stage_block<MAXE>(p, ref, slot_of(k), stage, meta, pc, lane, spec_acc);
       mark(3);
-      if (!(p.ablate & 1))
+      if (!ABLATE(p, 1))
         store3(p.lb + (uint64_t)b * 8, tag, readlane(pc.sc, 0), readlane(pc.sc, 1),
                readlane(pc.sc, 2), lane);
     }
     // e. group duty for the PREVIOUS block, one iteration late: its group's aggregates are
     // published by now (no spinning), and the duty never delays this block's aggregate
-    if (k >= 1 && k - 1 < KW && !(p.ablate & 1)) {
+    if (k >= 1 && k - 1 < KW && !ABLATE(p, 1)) {
       const uint32_t b = blk_of(k - 1);
       const uint32_t g0 = b & ~63u;
       const uint32_t gsize = (nblk - g0 < 64u) ? (nblk - g0) : 64u;
@@ -1208,7 +1208,7 @@ static int resident_per_cu(const DecodeParams& p, int num_cus, hipStream_t s) {
   (void)hipFree(c);
   per_cu = found;
   per_cu_cached.store(per_cu, std::memory_order_release);
-  if (getenv("LSMGPU_DEBUG"))
+  if (getenv("LSMGPU_DEBUG_ERR"))
     fprintf(stderr, "[lsmgpu] decode SLOT=%d census: api %d lds %d -> resident %d per CU\n", SLOT,
             api, Cfg::kLds, per_cu);
   return per_cu;
@@ -1232,12 +1232,11 @@ static hipError_t launch_cfg(const DecodeParams& p, int num_cus, hipStream_t s,
   if (grid > p.nblk) grid = p.nblk;  // one round: every block has its own workgroup
   if (grid < 1) grid = 1;
   *waves_launched = grid;
-  static const uint32_t ablate =
-      getenv("LSMGPU_ABLATE") ? (uint32_t)atoi(getenv("LSMGPU_ABLATE")) : 0u;
   DecodeParams q = p;
-  q.ablate = ablate;
   q.census = nullptr;
   q.stamps = nullptr;
+#ifdef LSMGPU_DIAG
+  q.ablate = getenv("LSMGPU_ABLATE") ? (uint32_t)atoi(getenv("LSMGPU_ABLATE")) : 0u;
   static uint64_t* stamps = nullptr;
   const bool want_stamps = getenv("LSMGPU_STAMPS") != nullptr;
   if (want_stamps) {
@@ -1250,8 +1249,10 @@ static hipError_t launch_cfg(const DecodeParams& p, int num_cus, hipStream_t s,
   if (getenv("LSMGPU_DEBUG"))
     fprintf(stderr, "[lsmgpu] decode %s SLOT=%d lds=%d per_cu=%d cus=%d grid=%llu nblk=%u\n",
             T::kName, T::kSlot, Cfg::kLds, per_cu, num_cus, (unsigned long long)grid, p.nblk);
+#endif
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64), Cfg::kLds, s, q);
   hipError_t e = hipGetLastError();
+#ifdef LSMGPU_DIAG
   if (e == hipSuccess && q.stamps) {
     uint64_t h[16] = {0};
     (void)hipMemcpyAsync(h, stamps, sizeof(h), hipMemcpyDeviceToHost, s);
@@ -1265,6 +1266,7 @@ static hipError_t launch_cfg(const DecodeParams& p, int num_cus, hipStream_t s,
     fprintf(stderr, "[lsmgpu] blocks by emit path: chunk %llu piece %llu global %llu\n",
             (unsigned long long)h[13], (unsigned long long)h[14], (unsigned long long)h[15]);
   }
+#endif
   return e;
 }
 

@@ -53,7 +53,7 @@ __device__ __forceinline__ void read_hdr_nt(const uint8_t* g, uint32_t& plen, ui
 
 // the same from a block staged in LDS at byte offset o (any alignment): three aligned dword
 // reads and two byte-aligns
-__device__ __forceinline__ void read_hdr_lds(const uint32_t* d, uint32_t o, uint32_t& plen,
+[[maybe_unused]] __device__ __forceinline__ void read_hdr_lds(const uint32_t* d, uint32_t o, uint32_t& plen,
                                              uint32_t& klen, uint32_t& vlen) {
   const uint32_t i = o >> 2, sh = o & 3u;
   const uint32_t w0 = d[i], w1 = d[i + 1], w2 = d[i + 2];
@@ -457,7 +457,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
   __shared__ uint32_t s_cb[3][kWave64 ? TB : 1];  // p.wscopy: each block's output bases
   __shared__ uint8_t s_mark[KEEP || !GW ? kWaves : 1][128];  // kWalkLaneView, p.wview: owner marks (lane + 1)
   // the staged walk copying its own blocks (p.wscopy): no records for a copy launch
-  const bool scopy = kWave64 && p.wscopy && !p.wfuse;
+  const bool scopy = kWave64 && LSMGPU_KNOB(p.wscopy, 0u) && !p.wfuse;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   // blocks per tile: TB, or for the wide lane walks p.wtbe <= TB (threads past it hold no block):
   // tiles sized so the two waves of tiles (one workgroup per CU) carry equal shares
@@ -516,7 +516,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
       bool staged = false;
       if ((uint64_t)off + len > p.data_len) {
         gst = LSMGPU_BLK_RANGE;
-      } else if (p.ablate & 4) {  // (timing-only ablation: no walk, every block empty)
+      } else if ABLATE(p, 4) {  // (timing-only ablation: no walk, every block empty)
       } else {
         const uint8_t* blk = p.data + off;
         // kStaged: the block's bytes [off, off + len) as (unaligned) 16-B chunks in the wave's
@@ -603,7 +603,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
           if constexpr (L == 64) {  // src is wave-uniform (from ballots)
             pos = __builtin_amdgcn_readlane(endq, src);
             shape = __builtin_amdgcn_readlane(klen | (vlen << 16), src);
-          } else if (L <= 16 && p.wdpp) {
+          } else if (L <= 16 && LSMGPU_KNOB(p.wdpp, 0u)) {
             // the group's OR of the one lane's values by DPP (quad swaps, half-row / row
             // mirrors) -- no LDS round trip on the round's dependent chain
             const bool me = k == src - gb;
@@ -633,7 +633,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
             __builtin_amdgcn_wave_barrier();  // the chunk is read before the next one fills
             if (acc && idx >= cend) row[idx & 31] = rec;
           }
-          if (p.wsub) {
+          if (LSMGPU_KNOB(p.wsub, 0u)) {
             a += m;
             if (a >= L) a = 0;
           }
@@ -716,7 +716,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
       if constexpr (!KEEP && !WIDE) s_off[tid] = off;  // the non-kept view epilogue's table
       lane_off = off;
     }
-    bool done = !valid || (p.ablate & 4);  // (timing-only ablation 4: no walk)
+    bool done = !valid || ABLATE(p, 4);  // (timing-only ablation 4: no walk)
     if (valid && (uint64_t)off + len > p.data_len) {
       st = LSMGPU_BLK_RANGE;
       done = true;
@@ -752,7 +752,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
       }
       // (timing-only ablation 128: no record flush; honoured only with ablation 2, under which
       // the copy reads no record -- a copy of stale records writes out of bounds)
-      if (!KEEP && (k & (CH - 1)) == CH - 1 && (p.ablate & 130) != 130) {
+      if (!KEEP && (k & (CH - 1)) == CH - 1 && ABLATE(p, 130) != 130) {
         const uint64_t fl = __ballot(rec);  // lanes holding records k-CH+1 .. k
         if (fl) {
           wave_lds_fence();
@@ -780,7 +780,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
       }
     }
     if (valid && !KEEP) row[n & (CH - 1)] = pos | (V << 16);
-    const uint64_t vm = KEEP || (p.ablate & 258) == 258 ? 0ull : __ballot(valid);  // (ablation 256: as 128)
+    const uint64_t vm = KEEP || ABLATE(p, 258) == 258 ? 0ull : __ballot(valid);  // (ablation 256: as 128)
     if (!KEEP) wave_lds_fence();
     constexpr uint32_t kPer = CH / 4;
 #pragma unroll
@@ -805,7 +805,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
   }
   __syncthreads();
   WSC_STAMP(1, __builtin_amdgcn_s_memrealtime());
-  if (p.wlbfull) {
+  if (LSMGPU_KNOB(p.wlbfull, 1u)) {
     // every tile publishes its aggregate; every thread sums some predecessors' (lookback_partial)
     uint32_t tn = 0, tk = 0, tv = 0;
     for (uint32_t w = 0; w < kWaves; w++) {
@@ -816,7 +816,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
     uint64_t* R = p.lb + (uint64_t)tile * 8;
     if (wave == 0) store3(R, p.tag, tn, tk, tv, lane);
     Tot part{0, 0, 0};
-    if (tile > 0 && !(p.ablate & 1)) part = lookback_partial(p.lb, tile, p.tag, tid, kThreads, p.result);
+    if (tile > 0 && !ABLATE(p, 1)) part = lookback_partial(p.lb, tile, p.tag, tid, kThreads, p.result);
     const uint32_t pn = wave_sum_sat(part.n), pk = wave_sum_sat(part.k), pv = wave_sum_sat(part.v);
     if (lane == 0) {
       s_part[wave][0] = pn;
@@ -846,7 +846,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
     }
     uint64_t* R = p.lb + (uint64_t)tile * 8;
     Tot ex{0, 0, 0};
-    if (tile > 0 && !(p.ablate & 1)) {  // (timing-only ablation 1: no look-back)
+    if (tile > 0 && !ABLATE(p, 1)) {  // (timing-only ablation 1: no look-back)
       store3(R, p.tag, tn, tk, tv, lane);
       ex = lookback(p.lb, tile, p.tag, lane, p.result);
     }
@@ -948,7 +948,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
       // (entry_outputs) the 68 MB cost 0.044 ms of C2's copy (profiles/r05r): its stores start
       // at every block's first entry, into lines shared with blocks copied on other XCDs.
       // Blocks with prefix-compressed entries keep them in the copy (copy_entries_plen).
-      if (p.weo && (p.mode & LSMGPU_MODE_MATERIALIZE)) {
+      if (LSMGPU_KNOB(p.weo, 0u) && (p.mode & LSMGPU_MODE_MATERIALIZE)) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // this wave's record flushes
         __builtin_amdgcn_wave_barrier();
         const bool valid = b < p.nblk;
@@ -1001,7 +1001,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
     return;
   }
   if constexpr (KEEP) {
-    if (!((p.mode & LSMGPU_MODE_VIEW) && p.view) || (p.ablate & 2)) return;  // mode 0: no view
+    if (!((p.mode & LSMGPU_MODE_VIEW) && p.view) || ABLATE(p, 2)) return;  // mode 0: no view
     // each wave writes its 64 blocks' records -- consecutive in the output -- one lane per
     // entry, 64 consecutive 8-B records per store instruction, from the rows its lanes filled
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // rows (and any spill) written
@@ -1027,7 +1027,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
       const uint32_t kl = (m1 & 0xffffu) - hp - 10 - vl;  // stored key bytes
       p.view[ew + f] = (uint64_t)(offL + hp + 10) | ((uint64_t)kl << 32) | ((uint64_t)vl << 48);
     };
-    if (p.wview) {
+    if (LSMGPU_KNOB(p.wview, 1u)) {
       // owners by one scatter and a max-scan, two passes (128 entries) per trip: every block
       // with entries marks (lane + 1) at its first entry's slot, a DPP max-scan carries the
       // marks forward (the previous pass's last owner carried in)
@@ -1079,7 +1079,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
     if (tid == kThreads - 1) s_first[kThreads] = rel + n;
   }
   __syncthreads();
-  if (!((p.mode & LSMGPU_MODE_VIEW) && p.view) || (p.ablate & 2)) return;  // mode 0: no view
+  if (!((p.mode & LSMGPU_MODE_VIEW) && p.view) || ABLATE(p, 2)) return;  // mode 0: no view
   const uint32_t nt = s_first[kThreads];
   const uint64_t e0 = s_ex[0];
   // entry -> block map in the walk's staging rows (free now): each thread marks its block's
@@ -1535,7 +1535,7 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
                                            bool duties) {
   const uint32_t st = sw & ~kPlenFlag;
   // duties: the per-block outputs, unless the walk kernel wrote them (every copy launch)
-  if (duties && lane == 0 && sub == 0 && !(p.ablate & 32)) {  // (timing-only ablation 32)
+  if (duties && lane == 0 && sub == 0 && !ABLATE(p, 32)) {  // (timing-only ablation 32)
     if (p.blk_first) p.blk_first[b] = (uint32_t)en;
     if (p.blk_status) p.blk_status[b] = (int32_t)st;
     if (st != LSMGPU_BLK_OK) {
@@ -1562,7 +1562,7 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
     if (duties && lane == 0 && sub == 0) atomicOr(reinterpret_cast<unsigned long long*>(p.result + 5), 1ull);
     return;
   }
-  if (n == 0 || (p.ablate & 2)) return;
+  if (n == 0 || ABLATE(p, 2)) return;
   const uint8_t* blk = p.data + off;  // (prefix-compressed blocks)
   uint8_t* kbase = p.key_data ? p.key_data + ek : nullptr;
   uint8_t* vbase = p.val_data ? p.val_data + ev : nullptr;
@@ -1582,31 +1582,31 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
   // (round 4: each lane's first piece of every entry of a pass loaded before any store left
   // the copy unchanged, 0.6038 vs 0.6042 ms, profiles/r04c; compiled into this kernel it also
   // raised the VGPRs from 44 to 90, 8 -> 5 waves per SIMD: removed)
-  if (p.walign == 2 && mat && split == 1 && n < kWave && tab && chunks_fit(kbase, vbase, K, V)) {
+  if (LSMGPU_KNOB(p.walign, 0u) == 2 && mat && split == 1 && n < kWave && tab && chunks_fit(kbase, vbase, K, V)) {
     // dense aligned chunks over both streams (copy_chunks)
-    if (!p.weo) entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
+    if (!LSMGPU_KNOB(p.weo, 0u)) entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
     const uint64_t lim = p.data_len - off;
     copy_chunks(blk, lim < 0xffffffffull ? (uint32_t)lim : 0xffffffffu, kbase, vbase, n, K, V, lane, pre, tab);
-  } else if (p.walign == 1 && mat && split == 1) {
+  } else if (LSMGPU_KNOB(p.walign, 0u) == 1 && mat && split == 1) {
     // aligned output chunks + the stream edges byte by byte (copy_entries_aligned)
-    if (!p.weo) entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
-    if (p.wj == 16 || (p.wj == 0 && avg > 128))
+    if (!LSMGPU_KNOB(p.weo, 0u)) entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
+    if (LSMGPU_KNOB(p.wj, 0u) == 16 || (LSMGPU_KNOB(p.wj, 0u) == 0 && avg > 128))
       copy_entries_aligned<16, 2>(meta, blk, kbase, vbase, n, K, V, sub, split, lane, pre);
     else
       copy_entries_aligned<8, 5>(meta, blk, kbase, vbase, n, K, V, sub, split, lane, pre);
-  } else if ((p.wj == 16 || (p.wj == 0 && avg > 128)) && (p.weo || p.weosep || !mat)) {
+  } else if ((LSMGPU_KNOB(p.wj, 0u) == 16 || (LSMGPU_KNOB(p.wj, 0u) == 0 && avg > 128)) && (LSMGPU_KNOB(p.weo, 0u) || LSMGPU_KNOB(p.weosep, 0u) || !mat)) {
     // (outputs: the walk wrote them, or one lane per entry first: a view-only decode through
     // the copy kernel (C5 view 0.270 -> 0.238 ms, profiles/r05ae), or LSMGPU_WSC_EOSEP=1 -- for
     // materialize the 16-lane groups' own writes stay faster: C5 copy 0.607 vs 0.617 ms, C3
     // 0.494-0.498 vs 0.508-0.510)
-    if (!p.weo && !(p.ablate & 8)) entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
+    if (!LSMGPU_KNOB(p.weo, 0u) && !ABLATE(p, 8)) entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
     copy_entries<16, 2, false>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
-  } else if (p.wj == 16 || (p.wj == 0 && avg > 128)) {
+  } else if (LSMGPU_KNOB(p.wj, 0u) == 16 || (LSMGPU_KNOB(p.wj, 0u) == 0 && avg > 128)) {
     copy_entries<16, 2, true>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
   } else {
     // (timing-only ablations: 8 no per-entry outputs, 16 no pieces)
-    if (!(p.ablate & 8) && !p.weo) entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
-    if (mat && !(p.ablate & 16))
+    if (!ABLATE(p, 8) && !LSMGPU_KNOB(p.weo, 0u)) entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
+    if (mat && !ABLATE(p, 16))
       copy_entries<8, 5, false>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
   }
 }
@@ -1684,7 +1684,7 @@ __global__ void __launch_bounds__(TB) wsc_walk_persist_kernel(DecodeParams p) {
       off = p.blk_off[b];
       len = p.blk_len[b];
     }
-    bool done = !valid || (p.ablate & 4);
+    bool done = !valid || ABLATE(p, 4);
     if (valid && (uint64_t)off + len > p.data_len) {
       st = LSMGPU_BLK_RANGE;
       done = true;
@@ -1779,7 +1779,7 @@ __global__ void __launch_bounds__(TB) wsc_walk_persist_kernel(DecodeParams p) {
     const uint32_t tile = tl[r];
     if (tile >= ntiles) continue;  // (uniform)
     Tot part{0, 0, 0};
-    if (tile > 0 && !(p.ablate & 1)) part = lookback_partial(p.lb, tile, p.tag, tid, kThreads, p.result);
+    if (tile > 0 && !ABLATE(p, 1)) part = lookback_partial(p.lb, tile, p.tag, tid, kThreads, p.result);
     const uint32_t pn = wave_sum_sat(part.n), pk = wave_sum_sat(part.k), pv = wave_sum_sat(part.v);
     if (lane == 0) {
       s_part[wave][0] = pn;
@@ -1838,13 +1838,22 @@ __global__ void __launch_bounds__(TB) wsc_walk_persist_kernel(DecodeParams p) {
 
 hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mid) {
   const uint32_t nblk = p.nblk;
-  const bool persist = p.wpersist && !p.wfuse && p.wwalk != kWalkGroup && p.wwide == 576 && p.wchunk == 32 && !p.weo;
+  // the adopted walks (api.hip picks one per batch; the parity suite runs each of them):
+  //   materialize, wide tiles (> 4 x 256-block tiles per CU): two 576-thread tiles per workgroup
+  //   view-only fused into the walk: kWalkLaneView, 576- or 256-block tiles
+  //   <= 64 blocks per CU: 8 lanes forward + 8 backward per block (kWalkGroupBi)
+  //   otherwise one lane per block, 256-block tiles
+  const bool persist = LSMGPU_KNOB(p.wpersist, 1u) && !p.wfuse && p.wwalk != kWalkGroup && p.wwide == 576 &&
+                       LSMGPU_KNOB(p.wchunk, 32u) == 32 && !LSMGPU_KNOB(p.weo, 0u);
   if (persist)
     hipLaunchKernelGGL(wsc_walk_persist_kernel<576>, dim3(((nblk + p.wtbe - 1) / p.wtbe + 1) / 2), dim3(576), 0, s, p);
+#ifdef LSMGPU_DIAG
   else if (p.wwalk == kWalkGroup && p.wlanes == 8 && p.wbidir == 2)  // 16 lanes forward + 16 backward
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroupBi, 8>), dim3((nblk + 7) / 8), dim3(256), 0, s, p);
-  else if (p.wwalk == kWalkGroup && p.wlanes == 8 && p.wbidir)  // 8 lanes forward + 8 backward
+#endif
+  else if (p.wwalk == kWalkGroup && p.wlanes == 8 && LSMGPU_KNOB(p.wbidir, 1u))  // 8 lanes forward + 8 backward
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroupBi, 16>), dim3((nblk + 15) / 16), dim3(256), 0, s, p);
+#ifdef LSMGPU_DIAG
   else if (p.wwalk == kWalkGroup && p.wlanes == 2)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 128>), dim3((nblk + 127) / 128), dim3(256), 0, s, p);
   else if (p.wwalk == kWalkGroup && p.wlanes == 4)
@@ -1861,14 +1870,18 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 16>), dim3((nblk + 15) / 16), dim3(256), 0, s, p);
   else if (p.wwalk == kWalkGroup)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 32>), dim3((nblk + 31) / 32), dim3(256), 0, s, p);
-  else if (p.wfuse && p.wkeep && p.wwide == 576)
+#endif
+  else if (p.wfuse && LSMGPU_KNOB(p.wkeep, 1u) && p.wwide == 576)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLaneView, 576>), dim3((nblk + p.wtbe - 1) / p.wtbe), dim3(576), 0, s, p);
+#ifdef LSMGPU_DIAG
   else if (!p.wfuse && p.wwide == 576 && p.wchunk == 32)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 576>), dim3((nblk + p.wtbe - 1) / p.wtbe), dim3(576), 0, s, p);
   else if (p.wfuse && p.wkeep && p.wtile == 192)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLaneView, 192>), dim3((nblk + 191) / 192), dim3(192), 0, s, p);
-  else if (p.wfuse && p.wkeep)
+#endif
+  else if (p.wfuse && LSMGPU_KNOB(p.wkeep, 1u))
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLaneView, 256>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
+#ifdef LSMGPU_DIAG
   else if (p.wchunk == 16)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 256, 16>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
   else if (p.wtile == 192)
@@ -1877,7 +1890,9 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
     (void)hipFuncSetAttribute((const void*)wsc_walk_kernel<kWalkLane, 256>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.wpad);
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 256>), dim3((nblk + 255) / 256), dim3(256), p.wpad, s, p);
-  } else
+  }
+#endif
+  else
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 256>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
   hipError_t e = hipGetLastError();
 #ifdef LSMGPU_STAMPS
@@ -1930,7 +1945,7 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
 #endif
   if (e == hipSuccess && mid) e = hipEventRecord(mid, s);
   // view-only, or the staged walk copying its blocks: the walk wrote everything
-  if (e != hipSuccess || p.wfuse || p.wscopy) return e;
+  if (e != hipSuccess || p.wfuse || LSMGPU_KNOB(p.wscopy, 0u)) return e;
   const uint32_t per_wg = 4 / p.wsplit;  // blocks per 4-wave workgroup
   hipLaunchKernelGGL(wsc_copy_kernel, dim3((nblk + per_wg - 1) / per_wg), dim3(256), 0, s, p);
   return hipGetLastError();

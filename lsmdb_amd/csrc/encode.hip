@@ -186,7 +186,7 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
       const uint64_t r = e0 + i * EPP + lane / J;
       const uint32_t prev = r == 0 ? 0xffffffffu : (lane < J ? edge : below) - bs;  // builder.go:95-99
       if (on[i] && j == 0) {
-        if (p.hdr16 && klen[i] >= 8) {  // (8-B key read inside the key)
+        if (LSMGPU_KNOB(p.hdr16, 1u) && klen[i] >= 8) {  // (8-B key read inside the key)
           // the header and the key's first 6 bytes as one 16-B store (the key's first piece
           // rewrites those 6 bytes with the same values): one store instruction per pass instead
           // of an 8-B and a 2-B one
@@ -322,24 +322,26 @@ hipError_t launch_encode(const EncodeParams& p0, int num_cus, hipStream_t s) {
   (void)num_cus;
   EncodeParams p = p0;
   // one 16-B store for the header and the key's first 6 bytes (same box, C2 encode 0.5864-0.5895
-  // -> 0.5627-0.5667 ms, profiles/r05ae); LSMGPU_ENC_HDR16=0: the 8-B + 2-B header stores
-  const char* h16 = getenv("LSMGPU_ENC_HDR16");
-  p.hdr16 = h16 && atoi(h16) == 0 ? 0u : 1u;
+  // -> 0.5627-0.5667 ms, profiles/r05ae); diag build: LSMGPU_ENC_HDR16=0 keeps the 8-B + 2-B stores
+  p.hdr16 = 1u;
   // J = lanes per entry ~ the average entry's 16-B pieces (C2: 129 B -> 8; C3: ~1.1 KB -> 64)
   const uint64_t avg = p.n ? (p.key_total + p.vs_total) / p.n : 120;
-  const char* ge = getenv("LSMGPU_ENC_G");  // A/B: entry-group passes per loop trip
-  const int g = ge ? atoi(ge) : 1;           // measured: C2 G=1 0.61 ms, 2 0.68, 4 0.72
-  const char* je = getenv("LSMGPU_ENC_J");   // A/B: lanes per entry
-  if (je) {
+  // LSMGPU_ENC_J (test hook): one of the compiled J (4, 8, 16) whatever the entry size
+  if (const char* je = getenv("LSMGPU_ENC_J")) {
     const int jj = atoi(je);
     if (jj == 4) return launch_enc<4, 1>(p, s);
     if (jj == 16) return launch_enc<16, 1>(p, s);
     if (jj == 8) return launch_enc<8, 1>(p, s);
   }
-  // measured (1 GiB): C2 (119 B entries) J=8 0.57 ms vs J=4 0.63 / J=16 0.73; C5 (~141 B)
-  // J=16 0.88 ms vs J=8 0.96
+#ifdef LSMGPU_DIAG
+  if (const char* h16 = getenv("LSMGPU_ENC_HDR16")) p.hdr16 = atoi(h16) == 0 ? 0u : 1u;
+  const char* ge = getenv("LSMGPU_ENC_G");  // A/B: entry-group passes per loop trip
+  const int g = ge ? atoi(ge) : 1;           // measured: C2 G=1 0.61 ms, 2 0.68, 4 0.72
   if (g == 4) return avg <= 128 ? launch_enc<8, 4>(p, s) : launch_enc<16, 4>(p, s);
   if (g == 2) return avg <= 128 ? launch_enc<8, 2>(p, s) : launch_enc<16, 2>(p, s);
+#endif
+  // measured (1 GiB): C2 (119 B entries) J=8 0.57 ms vs J=4 0.63 / J=16 0.73; C5 (~141 B)
+  // J=16 0.88 ms vs J=8 0.96
   if (avg <= 48) return launch_enc<4, 1>(p, s);
   if (avg <= 128) return launch_enc<8, 1>(p, s);
   if (avg <= 496) return launch_enc<16, 1>(p, s);

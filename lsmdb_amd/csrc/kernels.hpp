@@ -7,6 +7,23 @@
 
 namespace lsmgpu {
 
+// Experiment knobs.  The product library (liblsmgpu.so) compiles only the adopted decode and
+// encode paths: every DecodeParams field marked "(diag)" below reads as its default there, and
+// the rejected variants are not instantiated.  The diagnostic build (LSMGPU_DIAG, built as
+// liblsmgpu_diag.so by `LSMGPU_BUILD_DIAG=1 python -m lsmdb_amd._build`) reads them from the
+// LSMGPU_WSC_* / LSMGPU_ENC_* / LSMGPU_ABLATE environment and keeps the per-phase stamps, for
+// the A/B records in DESIGN.md.
+#ifdef LSMGPU_DIAG
+#ifndef LSMGPU_STAMPS
+#define LSMGPU_STAMPS 1
+#endif
+#define LSMGPU_KNOB(v, dflt) (v)
+#else
+#define LSMGPU_KNOB(v, dflt) (dflt)
+#endif
+// timing-only ablation bits (diag): 0 in the product library
+#define ABLATE(p, m) LSMGPU_KNOB(((p).ablate & (m)), 0u)
+
 // Decode: one-wave workgroups over a persistent, fully resident grid, one SST data block per
 // iteration, software-pipelined (walk block k, emit block k-2); output bases from a two-level
 // prefix over per-block {entries, key bytes, value bytes}.  DESIGN.md.

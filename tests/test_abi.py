@@ -38,7 +38,7 @@ def test_exports_via_nm():
 
 def test_version_and_strerror():
     lib = _lib.lib()
-    assert lib.lsmgpu_abi_version() == 3
+    assert lib.lsmgpu_abi_version() == 4
     for code in range(0, 12):
         assert lib.lsmgpu_strerror(code)
     assert lib.lsmgpu_strerror(_lib.ERR_CAPACITY) == b"output buffer too small"

@@ -4,7 +4,12 @@ chunks (copy-in / decode / copy-out on three streams, api.hip decode_host_pipeli
 sizes of 1-3 MiB (LSMGPU_HOST_CHUNK) cut the test inputs into many chunks, so the per-chunk
 bases, the block-index and status arrays across chunk borders, the first bad block and the
 capacity rules are all exercised; every output is checked against the oracle.  Unsorted block
-lists and chunks whose prefix-compressed keys outgrow their device slot take the one-shot path."""
+lists and chunks whose prefix-compressed keys outgrow their device slot take the one-shot path.
+
+ABI 4 (host_io.hpp): pageable input and outputs are staged through the ctx's own page-locked
+buffers; lsmgpu_host_alloc memory is DMA'd directly.  Both sides are run in every combination.
+lsmgpu_host_register pins nothing any more; the register / unregister / re-use cycles that
+faulted in round 5 (GPUTEST_r05) stay here as the regression test of that fix."""
 from ctypes import byref
 
 import numpy as np
@@ -58,29 +63,59 @@ def _check(g, ref, m, what):
 @pytest.mark.parametrize("chunk", ["1048576", "3000000"])
 @pytest.mark.parametrize("mode", ["both", "view", "materialize"])
 def test_host_pipeline_vs_oracle(codec, mixed, monkeypatch, chunk, mode):
-    """Pageable and pinned input, pinned per test (register -> decode -> unregister) on a fresh
-    buffer: the allocator hands back pages of earlier tests' buffers, as compaction's
-    OpenTable / DecrRef cycles do (levels.go:281-298, table/table.go:53-71)."""
+    """Input pageable, registered (register -> decode -> unregister on a fresh buffer: the
+    allocator hands back pages of earlier tests' buffers, as compaction's OpenTable / DecrRef
+    cycles do, levels.go:281-298, table/table.go:53-71) or in host_alloc memory; outputs pageable
+    or in host_alloc memory: the staged and the direct DMA branches of both copy directions."""
     monkeypatch.setenv("LSMGPU_HOST_CHUNK", chunk)
     data, off, ln, ref = mixed
     m = {"both": MODE_MATERIALIZE | MODE_VIEW, "view": MODE_VIEW, "materialize": MODE_MATERIALIZE}[mode]
-    for pinned in (False, True):
-        buf = np.frombuffer(data, np.uint8).copy()
-        if pinned:
-            codec.host_register(buf)
-        try:
-            g = codec.decode_host(buf, off, ln, mode=m)
-        finally:
-            if pinned:
-                codec.host_unregister(buf)
-        _check(g, ref, m, f"chunk={chunk} pinned={pinned}")
+    for src in ("pageable", "registered", "host_alloc"):
+        for pinned_out in (False, True):
+            if src == "host_alloc":
+                buf = codec.host_alloc(len(data))
+                buf[:] = np.frombuffer(data, np.uint8)
+            else:
+                buf = np.frombuffer(data, np.uint8).copy()
+            if src == "registered":
+                codec.host_register(buf)
+            try:
+                g = codec.decode_host(buf, off, ln, mode=m, pinned_out=pinned_out)
+            finally:
+                if src == "registered":
+                    codec.host_unregister(buf)
+            _check(g, ref, m, f"chunk={chunk} src={src} pinned_out={pinned_out}")
+
+
+def test_host_churn_reused_addresses(codec, mixed, monkeypatch):
+    """Compaction's OpenTable / DecrRef churn (levels.go:281-298, table/table.go:53-71,117-123):
+    40 rounds of allocate -> register -> decode -> unregister -> free, at random sizes and
+    misalignments, so buffers come back at addresses earlier rounds used (the round-5 fault,
+    GPUTEST_r05); every round checked against the oracle.  Registration pins nothing: registering
+    the same range twice is accepted (the runtime does not see it as page-locked)."""
+    monkeypatch.setenv("LSMGPU_HOST_CHUNK", "1048576")
+    data, off, ln, ref = mixed
+    rng = np.random.default_rng(11)
+    n = len(data)
+    for r in range(40):
+        pad = int(rng.integers(0, 8192))
+        raw = np.empty(n + pad + int(rng.integers(0, 3 << 20)), np.uint8)
+        buf = raw[pad:pad + n]
+        buf[:] = np.frombuffer(data, np.uint8)
+        codec.host_register(buf)
+        assert _lib.lib().lsmgpu_host_register(codec._ctx, _ptr(buf), buf.nbytes) == _lib.OK
+        g = codec.decode_host(buf, off, ln, pinned_out=bool(r % 3 == 2))
+        codec.host_unregister(buf)
+        codec.host_unregister(buf)
+        _check(g, ref, 3, f"churn round {r}")
+        del raw, buf, g
 
 
 def test_host_register_shared_pages(codec, mixed, monkeypatch):
     """Two non-page-aligned copies of the input in one allocation, 16 B apart (a page shared by
     both, as Go heap buffers under LoadToRAM share pages, table/table.go:117-123,329-338): both
-    pinned, both decoded, the first unpinned (its segment is re-cut: the second still needs the
-    shared page) and the second decoded again, then unpinned."""
+    registered, both decoded, the first unregistered and the second decoded again, then
+    unregistered, then the first decoded unregistered."""
     monkeypatch.setenv("LSMGPU_HOST_CHUNK", "1048576")
     data, off, ln, ref = mixed
     n = len(data)
@@ -101,9 +136,10 @@ def test_host_register_shared_pages(codec, mixed, monkeypatch):
 
 
 def test_host_register_cycles_and_nesting(codec, mixed, monkeypatch):
-    """register / unregister / register again at one address; a sub-range registered inside a
-    pinned range (no new pin) and decoded at an unaligned pointer; unregistering in either order;
-    an unknown pointer is LSMGPU_ERR_ARG."""
+    """register / unregister / register again at one address (the round-5 fault: GPUTEST_r05,
+    illegal address on the first D2H of this test); a sub-range registered inside a registered
+    range and decoded at an unaligned pointer; unregistering in either order; an unknown pointer
+    is LSMGPU_ERR_ARG."""
     monkeypatch.setenv("LSMGPU_HOST_CHUNK", "1048576")
     data, off, ln, ref = mixed
     buf = np.zeros(len(data) + 4096 + 13, np.uint8)
@@ -125,7 +161,7 @@ def test_host_register_cycles_and_nesting(codec, mixed, monkeypatch):
 
 def test_host_register_readonly_mmap(codec, oracle, tmp_path, monkeypatch):
     """A real .sst file mmap'd read-only (MemoryMap mode, table/table.go:88-144, y/mmap.go:11-21)
-    is pinned read-only, decoded through the pipeline and unpinned."""
+    is registered, decoded through the pipeline (staged) and unregistered."""
     import mmap
     monkeypatch.setenv("LSMGPU_HOST_CHUNK", "1048576")
     c2 = _cols(2, 60000, seed=71)
@@ -150,7 +186,7 @@ def test_host_register_readonly_mmap(codec, oracle, tmp_path, monkeypatch):
 
 def test_host_register_foreign_pinned(codec, mixed, monkeypatch):
     """Memory page-locked outside the library (torch's pinned allocator, hipHostMalloc) is not
-    registered again: LSMGPU_ERR_HOST_PINNED, and it decodes as it is."""
+    registered: LSMGPU_ERR_HOST_PINNED, and it decodes as it is (direct DMA)."""
     import torch
     monkeypatch.setenv("LSMGPU_HOST_CHUNK", "1048576")
     data, off, ln, ref = mixed
