@@ -142,7 +142,7 @@ int lsmgpu_decode_blocks(lsmgpu_ctx* ctx, const uint8_t* data, uint64_t data_len
  * directly at PCIe rate; any other host memory (a Go heap buffer under LoadToRAM,
  * table.go:117-123,329-338; an mmap'd .sst, y/mmap.go:11-21; pageable output arrays) is staged
  * through page-locked buffers the ctx owns, filled and drained by memcpy on a small per-ctx
- * thread pool (LSMGPU_COPY_THREADS, default min(8, hardware threads)).  So a caller that wants
+ * thread pool (LSMGPU_COPY_THREADS, default half the hardware threads, at most 16).  So a caller that wants
  * one copy of a table end to end reads the file into lsmgpu_host_alloc memory.
  * Every host call has finished all DMA into or out of caller memory when it returns. */
 int lsmgpu_host_alloc(lsmgpu_ctx* ctx, uint64_t bytes, void** out);  /* hipHostMalloc, portable */

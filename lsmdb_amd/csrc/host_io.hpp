@@ -161,11 +161,13 @@ class Stager {
   int next_ = 0;
 };
 
-// Copy-pool size: LSMGPU_COPY_THREADS, else up to 8 of the machine's hardware threads.
+// Copy-pool size: LSMGPU_COPY_THREADS, else half the machine's hardware threads, at most 16
+// (C2 1 GiB from pageable memory, materialize: 8 threads 0.035 s, 16 threads 0.026 s against a
+// 0.0186 s PCIe bound; profiles/r06b)
 inline unsigned copy_threads() {
   if (const char* e = getenv("LSMGPU_COPY_THREADS")) return (unsigned)std::max(1, atoi(e));
   const unsigned hw = std::thread::hardware_concurrency();
-  return std::max(1u, std::min(8u, hw ? hw : 1u));
+  return std::max(1u, std::min(16u, hw / 2));
 }
 
 }  // namespace lsmgpu

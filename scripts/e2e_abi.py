@@ -1,11 +1,13 @@
 """End-to-end decode through the C ABI from host memory (SURVEY §8(d) "End-to-end"; the drop-in
-path of an mmap'd .sst, table/table.go:88-144,153-166): lsmgpu_decode_blocks with
-data_on_device = 0 over the C2 1 GiB shard held in page-locked host memory
-(lsmgpu_host_register, what a cgo caller does to its mmap), outputs in registered host arrays.
+path of an OpenTable'd .sst, table/table.go:88-144,153-166): lsmgpu_decode_blocks with
+data_on_device = 0 over the C2 1 GiB shard, for two kinds of caller memory (ABI 4):
+  pageable   -- a Go heap buffer under LoadToRAM / an mmap, and pageable output arrays: the library
+                stages both directions through its own page-locked buffers (memcpy by its copy pool);
+  host_alloc -- input and outputs in lsmgpu_host_alloc memory: DMA'd directly.
 The library pipelines chunks (copy-in / decode / copy-out on three streams).  Reported beside the
-PCIe bound measured on the same box with the same buffers: hipMemcpyAsync of the input H2D, of
-the outputs D2H, and both at once on two streams.  The outputs are checked against a
-device-resident decode of the same blocks.  Prints one JSON line.
+PCIe bound measured on the same box with page-locked buffers: hipMemcpyAsync of the input H2D, of
+the outputs D2H.  The outputs are checked against a device-resident decode of the same blocks.
+Prints one JSON line.
 
     python scripts/e2e_abi.py [--reps N] [--chunk-mib M]
 """
@@ -77,20 +79,22 @@ def main():
     del ref, w
     torch.cuda.empty_cache()
 
-    # the caller's buffers, page-locked once (an mmap'd .sst would be registered read-only)
     ecap = data_len // 10 + 1
-    outs = dict(kd=np.empty(data_len, np.uint8), vd=np.empty(data_len, np.uint8),
-                ke=np.empty(ecap, np.uint32), ve=np.empty(ecap, np.uint32),
-                view=np.empty(ecap, np.uint64), bf=np.empty(nblk + 1, np.uint32),
-                bs=np.empty(nblk, np.int32))
-    t0 = time.perf_counter()
-    codec.host_register(host)
-    for a in outs.values():
-        codec.host_register(a)
-    reg_s = time.perf_counter() - t0
+    sizes = dict(kd=(data_len, np.uint8), vd=(data_len, np.uint8), ke=(ecap, np.uint32),
+                 ve=(ecap, np.uint32), view=(ecap, np.uint64), bf=(nblk + 1, np.uint32),
+                 bs=(nblk, np.int32))
     L = _lib.lib()
 
-    def decode(mode):
+    def buffers(kind):
+        def arr(nel, dt):
+            if kind == "pageable":
+                return np.empty(nel, dt)
+            return codec.host_alloc(nel * np.dtype(dt).itemsize).view(dt)[:nel]
+        h = arr(data_len, np.uint8)
+        h[:] = host
+        return h, {k: arr(*v) for k, v in sizes.items()}
+
+    def decode(src, outs, mode):
         d = _lib.LsmgpuDecoded()
         mat = mode & MODE_MATERIALIZE
         d.key_data, d.key_cap = (_ptr(outs["kd"]), data_len) if mat else (None, 0)
@@ -99,26 +103,29 @@ def main():
         d.val_end = _ptr(outs["ve"]) if mat else None
         d.view = _ptr(outs["view"]) if mode & MODE_VIEW else None
         d.ent_cap, d.blk_first, d.blk_status = ecap, _ptr(outs["bf"]), _ptr(outs["bs"])
-        rc = L.lsmgpu_decode_blocks(codec._ctx, _ptr(host), data_len, 0, _ptr(off), _ptr(ln), nblk,
+        rc = L.lsmgpu_decode_blocks(codec._ctx, _ptr(src), data_len, 0, _ptr(off), _ptr(ln), nblk,
                                     mode, byref(d))
         assert rc == _lib.OK, rc
         assert d.n_entries == n
         return d
 
     res = {}
-    for name, mode in (("view", MODE_VIEW), ("materialize", MODE_MATERIALIZE)):
-        s = median_s(lambda: decode(mode), args.reps)
-        if mode & MODE_VIEW:
-            assert np.array_equal(outs["view"][:n], want["view"]), "view parity"
-        else:
-            assert np.array_equal(outs["ke"][:n], want["ke"]) and np.array_equal(outs["ve"][:n], want["ve"])
-            assert np.array_equal(outs["kd"][:kt], want["kd"]) and np.array_equal(outs["vd"][:vt], want["vd"])
-        assert np.array_equal(outs["bf"], want["bf"]), "blk_first parity"
-        back = n * 8 + nblk * 8 if mode & MODE_VIEW else kt + vt + 8 * n + nblk * 8
-        res[name] = dict(seconds=round(s, 5), input_gibs=round(data_len / s / (1 << 30), 2),
-                         bytes_in=data_len, bytes_out=back)
-
-    # the PCIe bound with the same registered buffers (a device buffer of the input's size)
+    for kind in ("pageable", "host_alloc"):
+        src, outs = buffers(kind)
+        for name, mode in (("view", MODE_VIEW), ("materialize", MODE_MATERIALIZE)):
+            s = median_s(lambda: decode(src, outs, mode), args.reps)
+            if mode & MODE_VIEW:
+                assert np.array_equal(outs["view"][:n], want["view"]), "view parity"
+            else:
+                assert np.array_equal(outs["ke"][:n], want["ke"]) and np.array_equal(outs["ve"][:n], want["ve"])
+                assert np.array_equal(outs["kd"][:kt], want["kd"]) and np.array_equal(outs["vd"][:vt], want["vd"])
+            assert np.array_equal(outs["bf"], want["bf"]), "blk_first parity"
+            back = n * 8 + nblk * 8 if mode & MODE_VIEW else kt + vt + 8 * n + nblk * 8
+            res[f"{kind}_{name}"] = dict(seconds=round(s, 5), input_gibs=round(data_len / s / (1 << 30), 2),
+                                         bytes_in=data_len, bytes_out=back)
+        del src, outs
+    host, outs = buffers("host_alloc")  # page-locked buffers for the PCIe bound
+    # the PCIe bound with page-locked buffers (a device buffer of the input's size)
     rt = hip_runtime()
     dbuf = torch.empty(data_len, dtype=torch.uint8, device=dev)
     dout = torch.empty(data_len, dtype=torch.uint8, device=dev)
@@ -158,13 +165,10 @@ def main():
         res[name]["frac_of_pcie_bound"] = round(bound / res[name]["seconds"], 4)
     res["pcie"] = dict(h2d_gbs=round(data_len / t_h2d / 1e9, 2),
                        d2h_gbs=round(data_len / median_s(d2h(data_len), args.reps) / 1e9, 2),
-                       host_register_s=round(reg_s, 3))
-    codec.host_unregister(host)
-    for a in outs.values():
-        codec.host_unregister(a)
+                       copy_threads=os.environ.get("LSMGPU_COPY_THREADS", "default"))
     print(json.dumps({"what": "E2E decode through lsmgpu_decode_blocks (data_on_device=0), C2 "
-                      f"{data_len} B, {nblk} blocks, {n} entries; host buffers registered; "
-                      "chunk " + os.environ.get("LSMGPU_HOST_CHUNK", "64 MiB default"),
+                      f"{data_len} B, {nblk} blocks, {n} entries; pageable (staged) and host_alloc "
+                      "(direct) caller memory; chunk " + os.environ.get("LSMGPU_HOST_CHUNK", "32 MiB default"),
                       **res}), flush=True)
     codec.close()
 
