@@ -2,7 +2,8 @@
 
 * decodeTable: parse_index size query -> allocate -> parse_index; newDecodedBatch with upper
   bounds -> decode_blocks (-> the reported needs and a second decode_blocks only on
-  LSMGPU_ERR_CAPACITY); optionally pinned for the call (decodeTablePinned).  Checked against the oracle's decode
+  LSMGPU_ERR_CAPACITY); the table's bytes pageable (an mmap / Go heap buffer: staged by the
+  library) or read into lsmgpu_host_alloc memory (loadToHost: direct DMA).  Checked against the oracle's decode
   of the same blocks (table/iterator.go:93-135).
 * finishBlocks: encode_blocks size query (out == NULL) -> allocate out_len -> encode_blocks.
   Checked byte for byte against the oracle Builder (table/builder.go:84-198).
@@ -29,10 +30,17 @@ def shim_decode_table(ctx, sst: bytes, pin: bool = False):
     """decodeTable step by step: tail parse, upper-bound buffers (entries <=
     data/10, key and value bytes <= data), one decode; on LSMGPU_ERR_CAPACITY (prefix-compressed
     keys that expand) the reported needs are allocated and the decode repeated.  pin: the
-    table's bytes page-locked around the decode (decodeTablePinned: register, decode, unregister).  Returns the host SoA, the final call's needs,
-    the block list and the number of decode calls made."""
+    table's bytes in lsmgpu_host_alloc memory (loadToHost, table.go:117-123,329-338 under
+    LoadToRAM), else pageable.  Returns the host SoA, the final call's needs, the block list and
+    the number of decode calls made."""
     L = _lib.lib()
-    base = np.frombuffer(sst + b"\0", np.uint8).copy()
+    hp = ctypes.c_void_p()
+    if pin:  # loadToHost
+        assert L.lsmgpu_host_alloc(ctx, len(sst) + 1, byref(hp)) == _lib.OK
+        base = np.frombuffer((ctypes.c_uint8 * (len(sst) + 1)).from_address(hp.value), np.uint8)
+        base[:len(sst)] = np.frombuffer(sst, np.uint8)
+    else:
+        base = np.frombuffer(sst + b"\0", np.uint8).copy()
     nblk, bo, bl = c_uint64(0), c_uint64(0), c_uint64(0)
     rc = L.lsmgpu_parse_index(_ptr(base), len(sst), None, None, 0, byref(nblk), byref(bo), byref(bl))
     assert rc in (_lib.OK, _lib.ERR_CAPACITY)
@@ -42,8 +50,6 @@ def shim_decode_table(ctx, sst: bytes, pin: bool = False):
                                 byref(bo), byref(bl)) == _lib.OK
     n = nblk.value
     data_end = int(off[n - 1]) + int(ln[n - 1]) if n else 0
-    pinned = pin and L.lsmgpu_host_register(ctx, _ptr(base), base.size) == _lib.OK
-    assert pinned == pin  # plain numpy memory: the registration succeeds
 
     def batch(entries, kbytes, vbytes):  # newDecodedBatch
         arrs = dict(kd=np.zeros(max(kbytes, 1), np.uint8), vd=np.zeros(max(vbytes, 1), np.uint8),
@@ -65,8 +71,9 @@ def shim_decode_table(ctx, sst: bytes, pin: bool = False):
         d, arrs = batch(d.n_entries, d.key_bytes, d.val_bytes)
         rc = L.lsmgpu_decode_blocks(ctx, _ptr(base), data_end, 0, _ptr(off), _ptr(ln), n, MAT_VIEW,
                                     byref(d))
-    if pinned:
-        assert L.lsmgpu_host_unregister(ctx, _ptr(base)) == _lib.OK
+    if pin:  # freeHost (Table.DecrRef)
+        del base
+        assert L.lsmgpu_host_free(ctx, hp) == _lib.OK
     assert rc == _lib.OK
     m = d.n_entries
     need = (d.n_entries, d.key_bytes, d.val_bytes, d.first_bad_block, d.n_bad_blocks)
