@@ -465,6 +465,13 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     p.wview = 1u;
 #ifdef LSMGPU_DIAG
     decode_diag_knobs(p, nblk, cus, max_blk_len, wk_env);
+    // group walks: the copy in the walk's launch (LSMGPU_WSC_COPYFUSE=1), by workgroups past the
+    // last walk ticket, each block copied once its tile is walked (only the 8 + 8 group walk)
+    const char* cf_env = getenv("LSMGPU_WSC_COPYFUSE");
+    p.wcopyfuse = p.wwalk == kWalkGroup && p.wlanes == 8 && p.wbidir == 1 && !p.wfuse &&
+                  cf_env && atoi(cf_env) == 1 ? 1u : 0u;
+    p.wncop = (uint32_t)std::min<uint64_t>((nblk + (p.wsplit == 1 ? 4 : 2) - 1) / (p.wsplit == 1 ? 4 : 2),
+                                           6 * cus);  // (6 per CU: with the walk, ~7 resident)
 #endif
     // d_result is zeroed by the walk kernel when a copy launch follows it (the copy's atomics
     // come after the kernel boundary): one operation fewer per decode.  A view-only decode
@@ -483,7 +490,7 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     HIPC(launch_decode_wsc(p, c->stream, c->ktime ? c->kev[1] : nullptr));
     if (c->ktime) HIPC(hipEventRecord(c->kev[2], c->stream));
     c->kvalid = c->ktime;
-    c->kfused = p.wfuse != 0;
+    c->kfused = p.wfuse != 0 || LSMGPU_KNOB(p.wcopyfuse, 0u) != 0;
     return LSMGPU_OK;
   }
   uint64_t waves = 0;

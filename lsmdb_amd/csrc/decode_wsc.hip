@@ -76,6 +76,43 @@ __device__ __forceinline__ uint32_t group_or(uint32_t x) {
 
 }  // namespace
 
+// Device-coherent record traffic for the group walk's fused copy (p.wcopyfuse): the records and
+// descriptors a walk workgroup writes are read by copy workgroups on other XCDs inside the same
+// launch, and the XCDs' L2s are not coherent with each other.  Agent-scope relaxed atomics (sc1)
+// write them through and read them past the L2s; an agent-scope release / acquire per tile
+// instead writes back / invalidates a whole L2 (measured: C4 0.121 ms against 0.067 for the
+// walk and copy launches).
+// (Measured and not adopted, so the product library stores the records plainly and never
+// fuses the copy: C4 0.081 ms fused against 0.068 ms for the two launches -- every tile of a
+// group walk finishes at about the same time, so the copy cannot start much earlier, and the
+// copy workgroups slow the walk's dependent rounds; profiles/r06e.)
+__device__ __forceinline__ void st_rec4(uint32_t* dst, uint4 v) {  // 16-B aligned
+#ifdef LSMGPU_DIAG
+  uint64_t* d = reinterpret_cast<uint64_t*>(dst);
+  __hip_atomic_store(d, (uint64_t)v.x | ((uint64_t)v.y << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(d + 1, (uint64_t)v.z | ((uint64_t)v.w << 32), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+#else
+  *reinterpret_cast<uint4*>(dst) = v;
+#endif
+}
+template <bool COH>
+__device__ __forceinline__ uint32_t ldm(const uint32_t* a) {
+  if constexpr (COH) return __hip_atomic_load(const_cast<uint32_t*>(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *a;
+}
+template <bool COH>
+__device__ __forceinline__ uint4 ld_desc(const uint4* a) {
+  if constexpr (COH) {
+    uint64_t* d = reinterpret_cast<uint64_t*>(const_cast<uint4*>(a));
+    const uint64_t x = __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t y = __hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_uint4((uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32));
+  } else {
+    return *a;
+  }
+}
+
 // Per-entry metadata of the walk: one u32 record {header pos | value offset << 16} per entry
 // (both < 64 KiB in a block < 64 KiB), entry n = the sentinel {stop pos | V << 16}.  The copy
 // derives the rest: value length = the next record's value offset minus this one's, stored key
@@ -91,13 +128,20 @@ __device__ __forceinline__ uint32_t group_or(uint32_t x) {
 // copy's header-reading path
 constexpr uint32_t kPlenFlag = 1u << 16;  // u32 per lane row: 32 records + 1 pad (bank spread)
 
+// (group walks only: coherent stores, see st_rec4)
 __device__ __forceinline__ void flush_meta(uint32_t* dst, const uint32_t* row, uint32_t cnt) {
   if (cnt == 32) {
 #pragma unroll
     for (int i = 0; i < 8; i++)
-      reinterpret_cast<uint4*>(dst)[i] = make_uint4(row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3]);
+      st_rec4(dst + 4 * i, make_uint4(row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3]));
   } else {
-    for (uint32_t i = 0; i < cnt; i++) dst[i] = row[i];
+    for (uint32_t i = 0; i < cnt; i++) {
+#ifdef LSMGPU_DIAG
+      __hip_atomic_store(dst + i, row[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+      dst[i] = row[i];
+#endif
+    }
   }
 }
 
@@ -245,8 +289,8 @@ __device__ __forceinline__ void bidir_fwd(const DecodeParams& p, const uint8_t* 
     rounds++;
     if (gn >= cend) {  // chunk [cend - 32, cend) complete: one full 128-B line
       __builtin_amdgcn_wave_barrier();
-      reinterpret_cast<uint4*>(meta + cend - 32)[k] =
-          make_uint4(row[4 * k], row[4 * k + 1], row[4 * k + 2], row[4 * k + 3]);
+      st_rec4(meta + cend - 32 + 4 * k,
+              make_uint4(row[4 * k], row[4 * k + 1], row[4 * k + 2], row[4 * k + 3]));
       __builtin_amdgcn_wave_barrier();  // the chunk is read before the next one fills
       if (acc && idx >= cend) row[idx & 31] = rec;
     }
@@ -291,8 +335,8 @@ __device__ __forceinline__ void bidir_fwd(const DecodeParams& p, const uint8_t* 
       gn += mc;
       if (gn >= cend) {
         __builtin_amdgcn_wave_barrier();
-        reinterpret_cast<uint4*>(meta + cend - 32)[k] =
-            make_uint4(row[4 * k], row[4 * k + 1], row[4 * k + 2], row[4 * k + 3]);
+        st_rec4(meta + cend - 32 + 4 * k,
+                make_uint4(row[4 * k], row[4 * k + 1], row[4 * k + 2], row[4 * k + 3]));
         __builtin_amdgcn_wave_barrier();
         if (on && idx >= cend) row[idx & 31] = rec;
       }
@@ -354,13 +398,22 @@ struct LdsBytes {
   }
 };
 
-template <typename Src>
+template <typename Src, bool COH = false>  // COH: records read with coherent loads (ldm)
 __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, const uint32_t* meta,
                                            uint32_t pre, uint32_t n, uint32_t K, uint32_t V,
                                            uint32_t sw, uint64_t en, uint64_t ek, uint64_t ev,
                                            uint32_t off, uint32_t sub, uint32_t split,
                                            uint32_t lane, const Src& src, uint32_t* tab = nullptr,
                                            bool duties = true);
+
+// A copy workgroup inside a group walk's launch (p.wcopyfuse): copier c of ncop takes 4-wave
+// groups of blocks c, c + ncop, ... (p.wsplit waves per block, as wsc_copy_kernel) and copies
+// each block once the walk workgroup of its tile has published the tile's descriptors (granule
+// 7 of the tile record = the launch tag, stored once every record and descriptor store of the
+// tile -- coherent stores, st_rec4 -- has completed).  Copiers exist only past the last walk ticket, so every tile they wait for
+// is already being walked by a running workgroup: no deadlock, whatever the residency.
+__device__ __forceinline__ void fused_copier(const DecodeParams& p, uint32_t c, uint32_t ncop,
+                                          uint32_t tb);
 
 // K1: lane = block; a workgroup = a tile of 256 consecutive blocks, tiles taken in ticket order
 // (p.gcnt[0]).  After the walk the workgroup scans its blocks' {entries, key bytes, value
@@ -466,13 +519,22 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
 #ifdef LSMGPU_STAMPS
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
+  // group walks with the copy fused (p.wcopyfuse): gridDim.x = tiles + copiers
+  const bool fcopy = GW && !kWave64 && LSMGPU_KNOB(p.wcopyfuse, 0u) && !p.wfuse;  // (diag)
+  const uint32_t draws = fcopy ? gridDim.x : ntiles;
   if (tid == 0) {
     const uint32_t t = atomicAdd(p.gcnt, 1u);
-    if (t == ntiles - 1) atomicExch(p.gcnt, 0u);  // every ticket is taken
+    if (t == draws - 1) atomicExch(p.gcnt, 0u);  // every ticket is taken
     s_tile = t;
   }
   __syncthreads();
   const uint32_t tile = s_tile;
+  if constexpr (GW && !kWave64) {
+    if (fcopy && tile >= ntiles) {  // (uniform) a copy workgroup
+      fused_copier(p, tile - ntiles, draws - ntiles, TB);
+      return;
+    }
+  }
 #ifdef LSMGPU_STAMPS
   WSC_STAMP(0, t_start);
 #endif
@@ -628,8 +690,8 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
           if (gn >= cend) {  // chunk [cend - 32, cend) complete: one full 128-B line
             __builtin_amdgcn_wave_barrier();
             for (uint32_t i = k; i < 8; i += L)
-              reinterpret_cast<uint4*>(meta + cend - 32)[i] =
-                  make_uint4(row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3]);
+              st_rec4(meta + cend - 32 + 4 * i,
+                      make_uint4(row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3]));
             __builtin_amdgcn_wave_barrier();  // the chunk is read before the next one fills
             if (acc && idx >= cend) row[idx & 31] = rec;
           }
@@ -680,8 +742,8 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
       const uint32_t gnl = (uint32_t)__shfl((int)gn, (int)gbl);
       wave_lds_fence();
       for (uint32_t i = kk; i < 8; i += LB)
-        reinterpret_cast<uint4*>(meta + (gnl & ~31u))[i] =
-            make_uint4(row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3]);
+        st_rec4(meta + (gnl & ~31u) + 4 * i,
+                make_uint4(row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3]));
       if (kk == 0) {
         s_res[0][g] = gn;
         s_res[1][g] = gK;
@@ -888,8 +950,13 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
           swb = st | (plen_b ? kPlenFlag : 0u);
           offb = lane_off;
         }
-        p.wdesc[2ull * b] = make_uint4(n, K, V, swb);
-        p.wdesc[2ull * b + 1] = make_uint4(en, ek, ev, offb);
+        if (fcopy) {  // read by copy workgroups of this launch (st_rec4)
+          st_rec4(reinterpret_cast<uint32_t*>(p.wdesc + 2ull * b), make_uint4(n, K, V, swb));
+          st_rec4(reinterpret_cast<uint32_t*>(p.wdesc + 2ull * b + 1), make_uint4(en, ek, ev, offb));
+        } else {
+          p.wdesc[2ull * b] = make_uint4(n, K, V, swb);
+          p.wdesc[2ull * b + 1] = make_uint4(en, ek, ev, offb);
+        }
       }
       // The per-block outputs, here for every decode (round 5; view-only decodes have no copy):
       // one thread per block writes consecutive words -- from the copy kernel, one lane per
@@ -995,6 +1062,15 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
           emit(c0 + lane, v0 - 1);
           emit(c0 + 64 + lane, v1 - 1);
         }
+      }
+    }
+    if constexpr (GW && !kWave64) {
+      if (fcopy) {  // the tile's descriptors and records are complete: release them to the copiers
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // every wave's stores complete
+        __syncthreads();
+        if (tid == 0)  // (every record / descriptor store was coherent and has completed)
+          __hip_atomic_store(p.lb + (uint64_t)tile * 8 + 7, (uint64_t)p.tag, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     WSC_STAMP(3, __builtin_amdgcn_s_memrealtime());
@@ -1141,15 +1217,16 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
 // view records -- with one lane per entry, 64 consecutive entries per store instruction (the
 // copy's J-lane entry groups wrote 8 consecutive words per instruction: C2 1 GiB, that cost
 // 0.06 ms of the copy's 0.51).  Wave `sub` of `split` takes chunks sub, sub + split, ...
+template <bool COH>
 __device__ __forceinline__ void entry_outputs(const DecodeParams& p, const uint32_t* meta,
                                               uint32_t n, uint64_t en, uint64_t ek, uint64_t ev,
                                               uint32_t off, uint32_t sub, uint32_t split,
                                               bool mat, bool view, uint32_t lane, uint32_t pre) {
   for (uint32_t c0 = sub * kWave; c0 < n; c0 += split * kWave) {
     const uint32_t e = c0 + lane;
-    const uint32_t m0 = c0 == 0 ? pre : meta[min(e, n)];
+    const uint32_t m0 = c0 == 0 ? pre : ldm<COH>(meta + min(e, n));
     const uint32_t nx = (uint32_t)__shfl((int)m0, (int)min(lane + 1, kWave - 1));
-    const uint32_t m1 = lane + 1 < kWave ? nx : meta[min(e + 1, n)];
+    const uint32_t m1 = lane + 1 < kWave ? nx : ldm<COH>(meta + min(e + 1, n));
     if (e >= n) continue;
     const uint32_t hp = m0 & 0xffffu, vo = m0 >> 16, hp1 = m1 & 0xffffu, vo1 = m1 >> 16;
     const uint32_t vl = vo1 - vo, kl = hp1 - hp - 10 - vl;
@@ -1161,7 +1238,7 @@ __device__ __forceinline__ void entry_outputs(const DecodeParams& p, const uint3
   }
 }
 
-template <uint32_t J, uint32_t G, bool EO, typename Src>  // EO: also the per-entry outputs
+template <uint32_t J, uint32_t G, bool EO, typename Src, bool COH = false>  // EO: also the per-entry outputs
 __device__ __forceinline__ void copy_entries(const DecodeParams& p, const uint32_t* meta,
                                              const Src& blk, uint8_t* kbase, uint8_t* vbase,
                                              uint32_t n, uint64_t en, uint64_t ek, uint64_t ev,
@@ -1183,8 +1260,8 @@ __device__ __forceinline__ void copy_entries(const DecodeParams& p, const uint32
         m0 = (uint32_t)__shfl((int)pre, (int)ec);
         m1 = (uint32_t)__shfl((int)pre, (int)ec + 1);
       } else {
-        m0 = meta[ec];
-        m1 = meta[ec + 1];
+        m0 = ldm<COH>(meta + ec);
+        m1 = ldm<COH>(meta + ec + 1);
       }
       hp[i] = m0 & 0xffffu;
       vo[i] = m0 >> 16;
@@ -1491,6 +1568,7 @@ __device__ __forceinline__ void copy_chunks(const uint8_t* blk, uint32_t lim, ui
 // format the iterator accepts): entries 64 at a time, lane = entry, plen read from the header,
 // key offsets by a wave scan of plen + stored key bytes; keys bytewise as baseKey[:plen] ++ diff
 // (iterator.go:98-100), values as 16-B pieces.  Whole wave; `sub` / `split` share the entries.
+template <bool COH>
 __device__ __forceinline__ void copy_entries_plen(const DecodeParams& p, const uint32_t* meta,
                                                const uint8_t* blk, uint8_t* kbase, uint8_t* vbase,
                                                uint32_t n, uint64_t en, uint64_t ek, uint64_t ev,
@@ -1500,7 +1578,7 @@ __device__ __forceinline__ void copy_entries_plen(const DecodeParams& p, const u
   for (uint32_t e0 = 0; e0 < n; e0 += kWave) {
     const uint32_t e = e0 + lane;
     const bool on = e < n;
-    const uint32_t m0 = meta[min(e, n)], m1 = meta[min(e + 1, n)];
+    const uint32_t m0 = ldm<COH>(meta + min(e, n)), m1 = ldm<COH>(meta + min(e + 1, n));
     const uint32_t hp = m0 & 0xffffu, vo = m0 >> 16;
     const uint32_t vl = (m1 >> 16) - vo, kl = (m1 & 0xffffu) - hp - 10 - vl;
     const uint32_t plen = on ? ((uint32_t)blk[hp] << 8) | blk[hp + 1] : 0u;
@@ -1526,7 +1604,7 @@ __device__ __forceinline__ void copy_entries_plen(const DecodeParams& p, const u
 // One block's share of the copy (wave `sub` of `split`): per-block outputs and result totals,
 // the capacity check, then the entries -- from the walk's records `meta` (`pre` = record `lane`),
 // the block's bytes read through `src` (prefix-compressed blocks always from global memory).
-template <typename Src>
+template <typename Src, bool COH>
 __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, const uint32_t* meta,
                                            uint32_t pre, uint32_t n, uint32_t K, uint32_t V,
                                            uint32_t sw, uint64_t en, uint64_t ek, uint64_t ev,
@@ -1572,7 +1650,7 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
   // (same-box A/B vs 4 groups: 0.799 -> 0.781 ms)
   // a block with prefix-compressed entries (flagged by the walk: no load of the sentinel here)
   if (sw & kPlenFlag) {
-    copy_entries_plen(p, meta, blk, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane);
+    copy_entries_plen<COH>(p, meta, blk, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane);
     return;
   }
   // small entries (8 lanes each): the per-entry outputs first, 64 entries per store instruction
@@ -1582,14 +1660,14 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
   // (round 4: each lane's first piece of every entry of a pass loaded before any store left
   // the copy unchanged, 0.6038 vs 0.6042 ms, profiles/r04c; compiled into this kernel it also
   // raised the VGPRs from 44 to 90, 8 -> 5 waves per SIMD: removed)
-  if (LSMGPU_KNOB(p.walign, 0u) == 2 && mat && split == 1 && n < kWave && tab && chunks_fit(kbase, vbase, K, V)) {
+  if (!COH && LSMGPU_KNOB(p.walign, 0u) == 2 && mat && split == 1 && n < kWave && tab && chunks_fit(kbase, vbase, K, V)) {
     // dense aligned chunks over both streams (copy_chunks)
-    if (!LSMGPU_KNOB(p.weo, 0u)) entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
+    if (!LSMGPU_KNOB(p.weo, 0u)) entry_outputs<COH>(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
     const uint64_t lim = p.data_len - off;
     copy_chunks(blk, lim < 0xffffffffull ? (uint32_t)lim : 0xffffffffu, kbase, vbase, n, K, V, lane, pre, tab);
-  } else if (LSMGPU_KNOB(p.walign, 0u) == 1 && mat && split == 1) {
+  } else if (!COH && LSMGPU_KNOB(p.walign, 0u) == 1 && mat && split == 1) {
     // aligned output chunks + the stream edges byte by byte (copy_entries_aligned)
-    if (!LSMGPU_KNOB(p.weo, 0u)) entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
+    if (!LSMGPU_KNOB(p.weo, 0u)) entry_outputs<COH>(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
     if (LSMGPU_KNOB(p.wj, 0u) == 16 || (LSMGPU_KNOB(p.wj, 0u) == 0 && avg > 128))
       copy_entries_aligned<16, 2>(meta, blk, kbase, vbase, n, K, V, sub, split, lane, pre);
     else
@@ -1599,15 +1677,15 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
     // the copy kernel (C5 view 0.270 -> 0.238 ms, profiles/r05ae), or LSMGPU_WSC_EOSEP=1 -- for
     // materialize the 16-lane groups' own writes stay faster: C5 copy 0.607 vs 0.617 ms, C3
     // 0.494-0.498 vs 0.508-0.510)
-    if (!LSMGPU_KNOB(p.weo, 0u) && !ABLATE(p, 8)) entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
-    copy_entries<16, 2, false>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
+    if (!LSMGPU_KNOB(p.weo, 0u) && !ABLATE(p, 8)) entry_outputs<COH>(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
+    copy_entries<16, 2, false, Src, COH>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
   } else if (LSMGPU_KNOB(p.wj, 0u) == 16 || (LSMGPU_KNOB(p.wj, 0u) == 0 && avg > 128)) {
-    copy_entries<16, 2, true>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
+    copy_entries<16, 2, true, Src, COH>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
   } else {
     // (timing-only ablations: 8 no per-entry outputs, 16 no pieces)
-    if (!ABLATE(p, 8) && !LSMGPU_KNOB(p.weo, 0u)) entry_outputs(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
+    if (!ABLATE(p, 8) && !LSMGPU_KNOB(p.weo, 0u)) entry_outputs<COH>(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
     if (mat && !ABLATE(p, 16))
-      copy_entries<8, 5, false>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
+      copy_entries<8, 5, false, Src, COH>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
   }
 }
 
@@ -1636,6 +1714,38 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
              s_chunk[threadIdx.x >> 6], false);
 }
 
+
+__device__ __forceinline__ void fused_copier(const DecodeParams& p, uint32_t c, uint32_t ncop,
+                                             uint32_t tb) {
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6, split = p.wsplit;
+  const uint32_t sub = wave % split, per = 4 / split;  // blocks per 4-wave group
+  const uint32_t ngroups = (p.nblk + per - 1) / per;
+  for (uint32_t g = c; g < ngroups; g += ncop) {
+    const uint32_t b = g * per + wave / split;
+    if (b >= p.nblk) break;  // (wave-uniform; later groups are further out)
+    // relaxed polls (an acquiring poll invalidates the XCD's L2 each time: C4 1.0 ms instead of
+    // 0.067); the tile's records and descriptors are then read with coherent loads (st_rec4)
+    const uint64_t* flag = p.lb + (uint64_t)(b / tb) * 8 + 7;
+    if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (uint64_t)p.tag) {
+      SpinBound bound;
+      do {
+        if (bound.expired()) {
+          flag_timeout(p.result, lane);
+          return;
+        }
+        __builtin_amdgcn_s_sleep(20);
+      } while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (uint64_t)p.tag);
+    }
+    const uint32_t* meta = p.wmeta + (uint64_t)b * p.wcap;
+    const uint32_t pre = ldm<true>(meta + min(lane, p.wcap - 1));
+    const uint4 d0 = ld_desc<true>(p.wdesc + 2ull * b), d1 = ld_desc<true>(p.wdesc + 2ull * b + 1);
+    const uint32_t n = uniform(d0.x), K = uniform(d0.y), V = uniform(d0.z), sw = uniform(d0.w);
+    const uint64_t en = uniform(d1.x), ek = uniform(d1.y), ev = uniform(d1.z);
+    const uint32_t off = uniform(d1.w);
+    copy_block<GlobalBytes, true>(p, b, meta, pre, n, K, V, sw, en, ek, ev, off, sub, split, lane,
+                                  GlobalBytes{p.data + off}, nullptr, false);
+  }
+}
 
 // The wide lane walk with two tiles per workgroup (LSMGPU_WSC_PERSIST=1, materialize decodes of
 // 576-thread tiles).  In wsc_walk_kernel each tile's workgroup waits for its predecessors'
@@ -1852,7 +1962,9 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroupBi, 8>), dim3((nblk + 7) / 8), dim3(256), 0, s, p);
 #endif
   else if (p.wwalk == kWalkGroup && p.wlanes == 8 && LSMGPU_KNOB(p.wbidir, 1u))  // 8 lanes forward + 8 backward
-    hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroupBi, 16>), dim3((nblk + 15) / 16), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroupBi, 16>),
+                       dim3((nblk + 15) / 16 + (LSMGPU_KNOB(p.wcopyfuse, 0u) && !p.wfuse ? p.wncop : 0u)),
+                       dim3(256), 0, s, p);
 #ifdef LSMGPU_DIAG
   else if (p.wwalk == kWalkGroup && p.wlanes == 2)
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkGroup, 128>), dim3((nblk + 127) / 128), dim3(256), 0, s, p);
@@ -1945,7 +2057,7 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
 #endif
   if (e == hipSuccess && mid) e = hipEventRecord(mid, s);
   // view-only, or the staged walk copying its blocks: the walk wrote everything
-  if (e != hipSuccess || p.wfuse || LSMGPU_KNOB(p.wscopy, 0u)) return e;
+  if (e != hipSuccess || p.wfuse || LSMGPU_KNOB(p.wscopy, 0u) || LSMGPU_KNOB(p.wcopyfuse, 0u)) return e;
   const uint32_t per_wg = 4 / p.wsplit;  // blocks per 4-wave workgroup
   hipLaunchKernelGGL(wsc_copy_kernel, dim3((nblk + per_wg - 1) / per_wg), dim3(256), 0, s, p);
   return hipGetLastError();

@@ -84,6 +84,10 @@ struct DecodeParams {
   uint32_t wsub;            // group walk: odd-shaped entries re-guessed inside a round
   uint32_t wview;           // kWalkLaneView: owners by scatter + max-scan (else binary search)
   uint32_t wdpp;            // group walk (<= 16 lanes): round results by DPP (else LDS shuffles)
+  // (diag) group walks: the copy runs in the walk's launch -- workgroups drawing a ticket past
+  // the tiles copy blocks as soon as their tile's descriptors are published (wncop of them)
+  uint32_t wcopyfuse;
+  uint32_t wncop;
 
 };
 

@@ -532,6 +532,7 @@ def test_wsc_lanes_per_entry(codec, oracle, monkeypatch, lanes):
 
 
 @pytest.mark.parametrize("walk", _variants(["lane", "lane576persist", "group_bidir"],
+                                           ["group_bidir_copyfuse"] +
                                            ["lane16", "lane192", "lane576", "lane_flush",
                                             "lane_viewsearch", "group", "group2", "group4",
                                             "group16", "group32", "group64", "group64_copy",
@@ -550,6 +551,9 @@ def test_wsc_walk_modes(codec, oracle, monkeypatch, walk, mode):
     from lsmdb_amd.codec import MODE_MATERIALIZE, MODE_VIEW
     monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
     monkeypatch.setenv("LSMGPU_WSC_BIDIR", "0")  # (the group walk's default adds a backward group)
+    if walk.endswith("_copyfuse"):  # (diag) the group walk with the copy in its launch
+        monkeypatch.setenv("LSMGPU_WSC_COPYFUSE", "1")
+        walk = walk[:-len("_copyfuse")]
     if walk.endswith("_lbwin"):  # the windowed decoupled look-back (LSMGPU_WSC_LOOKBACK=window)
         monkeypatch.setenv("LSMGPU_WSC_LOOKBACK", "window")
         walk = walk[:-len("_lbwin")]
@@ -686,6 +690,7 @@ def _block_entries(block):
 
 
 @pytest.mark.parametrize("walk", _variants(["lane", "lane576p", "group_bidir"],
+                                           ["group_bidir_copyfuse"] +
                                            ["lane16", "lane192", "lane576", "group", "group32",
                                             "group64", "group64g", "group_sub", "group_bidir16"]))
 @pytest.mark.parametrize("mode", ["materialize", "view"])
@@ -701,6 +706,9 @@ def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
     from lsmdb_amd.codec import MODE_MATERIALIZE, MODE_VIEW
     monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
     # lane576p: the persistent two-tile walk (LSMGPU_WSC_PERSIST=1, 64-block tiles)
+    if walk.endswith("_copyfuse"):  # (diag) the group walk with the copy in its launch
+        monkeypatch.setenv("LSMGPU_WSC_COPYFUSE", "1")
+        walk = walk[:-len("_copyfuse")]
     monkeypatch.setenv("LSMGPU_WSC_PERSIST", "1" if walk == "lane576p" else "0")
     monkeypatch.setenv("LSMGPU_WSC_TBE", "1" if walk == "lane576p" else "0")
     walk = "lane576" if walk == "lane576p" else walk
@@ -779,10 +787,12 @@ def test_walk_adversarial(codec, oracle, monkeypatch, walk, mode):
 def test_kernel_times(codec, oracle, monkeypatch):
     """lsmgpu_set_kernel_timing / lsmgpu_kernel_times: no times before a timed walk-scan-copy
     decode; afterwards a positive walk and copy time (copy 0 for a view-only decode that ends
-    in the walk), and the timed decode's output is unchanged."""
+    in the walk, and -- diagnostic build -- for a group walk with its copy in the same launch), and the timed decode's
+    output is unchanged."""
     from lsmdb_amd.codec import MODE_VIEW
     monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
     monkeypatch.setenv("LSMGPU_WSC_VIEWFUSE", "1")
+
     c2 = _cols(2, 40000, seed=41)
     data, off, ln = _sst_blocks(oracle, [oracle.build_cols(c2.keys, c2.key_end, c2.vs, c2.vs_end,
                                                            0, 4096)[0]])
@@ -797,6 +807,12 @@ def test_kernel_times(codec, oracle, monkeypatch):
         codec.decode_host(data, off, ln, mode=MODE_VIEW)
         walk, copy = codec.kernel_times()
         assert walk > 0 and copy == 0
+        if DIAG:  # the group walk with the copy in its launch (diagnostic build)
+            monkeypatch.setenv("LSMGPU_WSC_COPYFUSE", "1")
+            _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln), "fused copy")
+            walk, copy = codec.kernel_times()
+            assert walk > 0 and copy == 0
+            monkeypatch.delenv("LSMGPU_WSC_COPYFUSE")
         monkeypatch.setenv("LSMGPU_DECODE_PATH", "lds")  # another path: no (stale) times
         codec.decode_host(data, off, ln)
         with pytest.raises(Exception):
