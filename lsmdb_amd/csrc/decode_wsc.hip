@@ -404,7 +404,7 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
                                            uint32_t sw, uint64_t en, uint64_t ek, uint64_t ev,
                                            uint32_t off, uint32_t sub, uint32_t split,
                                            uint32_t lane, const Src& src, uint32_t* tab = nullptr,
-                                           bool duties = true);
+                                           bool duties = true, uint8_t* mk = nullptr);
 
 // A copy workgroup inside a group walk's launch (p.wcopyfuse): copier c of ncop takes 4-wave
 // groups of blocks c, c + ncop, ... (p.wsplit waves per block, as wsc_copy_kernel) and copies
@@ -1601,6 +1601,71 @@ __device__ __forceinline__ void copy_entries_plen(const DecodeParams& p, const u
   }
 }
 
+// The entries of one block with no prefix-compressed entry, DENSE (round 6; blocks of large
+// entries, average > 128 B: C5's Zipf keys, C3): 64 entries at a time, one per lane, write their
+// per-entry outputs (64 consecutive words per store instruction) and count their 16-B pieces
+// (key pieces then value pieces, pieces16); a wave scan gives each entry its first piece, and
+// then every lane takes one piece of the run -- piece P's entry is the last one starting at or
+// before P: each entry marks (lane + 1) at its first piece's slot of the 64-piece window (mk:
+// 64 B of LDS per wave) and a DPP max-scan carries the owners forward.  The 16-lane groups this
+// replaces left a Zipf entry's idle lanes empty in every store (C5: 4.73 M store instructions
+// per 1 GiB copy against C2's 2.00 M for the same bytes).
+template <bool COH, typename Src>
+__device__ __forceinline__ void copy_entries_dense(const DecodeParams& p, const uint32_t* meta,
+                                                   const Src& blk, uint8_t* kbase, uint8_t* vbase,
+                                                   uint32_t n, uint64_t en, uint64_t ek, uint64_t ev,
+                                                   uint32_t off, uint32_t sub, uint32_t split,
+                                                   bool mat, bool view, uint32_t lane, uint32_t pre,
+                                                   uint8_t* mk) {
+  for (uint32_t c0 = sub * kWave; c0 < n; c0 += split * kWave) {
+    const uint32_t e = c0 + lane;
+    const uint32_t m0 = c0 == 0 ? pre : ldm<COH>(meta + min(e, n));
+    const uint32_t nx = (uint32_t)__shfl((int)m0, (int)min(lane + 1, kWave - 1));
+    const uint32_t m1 = lane + 1 < kWave ? nx : ldm<COH>(meta + min(e + 1, n));
+    const bool on = e < n;
+    const uint32_t hp = m0 & 0xffffu, vo = m0 >> 16, hp1 = m1 & 0xffffu, vo1 = m1 >> 16;
+    const uint32_t vl = vo1 - vo, kl = hp1 - hp - 10 - vl;  // stored key bytes
+    const uint32_t ko = hp - 10 * e - vo;                   // (no prefix-compressed entry here)
+    if (on) {
+      if (mat) {
+        if (p.key_end) p.key_end[en + e] = (uint32_t)(ek + ko + kl);
+        if (p.val_end) p.val_end[en + e] = (uint32_t)(ev + vo1);
+      }
+      if (view) p.view[en + e] = (uint64_t)(off + hp + 10) | ((uint64_t)kl << 32) | ((uint64_t)vl << 48);
+    }
+    if (!mat) continue;
+    const uint32_t kp = on && kbase ? pieces16(kl) : 0u;
+    const uint32_t pc = on ? kp + (vbase ? pieces16(vl) : 0u) : 0u;
+    const uint32_t ps = wave_scan_sat(pc, lane), ex = ps - pc;
+    const uint32_t T = __builtin_amdgcn_readlane(ps, 63);
+    uint32_t carry = 0;
+    for (uint32_t r0 = 0; r0 < T; r0 += kWave) {
+      mk[lane] = 0;
+      wave_lds_fence();
+      if (pc > 0 && ex >= r0 && ex < r0 + kWave) mk[ex - r0] = (uint8_t)(lane + 1);
+      wave_lds_fence();
+      const uint32_t own = max(wave_scan_max(mk[lane], lane), carry);  // 1 + the owner lane
+      carry = __builtin_amdgcn_readlane(own, 63);
+      wave_lds_fence();  // (the marks are read before the next window clears them)
+      const uint32_t L = own - 1;  // own >= 1: entry 0's first piece is piece 0
+      // the owner's fields, packed 16 + 16 bits (every one < 64 KiB in a block < 64 KiB)
+      const uint32_t a = (uint32_t)__shfl((int)(hp | (kl << 16)), (int)L);
+      const uint32_t c = (uint32_t)__shfl((int)(ko | (vo << 16)), (int)L);
+      const uint32_t d = (uint32_t)__shfl((int)(vl | (kp << 16)), (int)L);
+      const uint32_t exL = (uint32_t)__shfl((int)ex, (int)L);
+      const uint32_t hL = a & 0xffffu, kL = a >> 16, koL = c & 0xffffu, voL = c >> 16;
+      const uint32_t vL = d & 0xffffu, kpL = d >> 16;
+      const uint32_t P = r0 + lane;
+      if (P >= T) continue;
+      const uint32_t q = P - exL;
+      if (q < kpL)
+        blk.piece(kbase + koL, hL + 10, kL, q);
+      else
+        blk.piece(vbase + voL, hL + 10 + kL, vL, q - kpL);
+    }
+  }
+}
+
 // One block's share of the copy (wave `sub` of `split`): per-block outputs and result totals,
 // the capacity check, then the entries -- from the walk's records `meta` (`pre` = record `lane`),
 // the block's bytes read through `src` (prefix-compressed blocks always from global memory).
@@ -1610,7 +1675,7 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
                                            uint32_t sw, uint64_t en, uint64_t ek, uint64_t ev,
                                            uint32_t off, uint32_t sub, uint32_t split,
                                            uint32_t lane, const Src& src, uint32_t* tab,
-                                           bool duties) {
+                                           bool duties, uint8_t* mk) {
   const uint32_t st = sw & ~kPlenFlag;
   // duties: the per-block outputs, unless the walk kernel wrote them (every copy launch)
   if (duties && lane == 0 && sub == 0 && !ABLATE(p, 32)) {  // (timing-only ablation 32)
@@ -1657,6 +1722,14 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
   // (C2: copy 0.504 -> 0.485 ms; C5 / C3 blocks of fewer, larger entries lose 3 % that way, so
   // their 16-lane groups keep writing them)
   const uint32_t avg = (K + V) / n;
+  // dense pieces for entries of 129-512 B on average (C5 copy 0.593 -> 0.547 ms); above that the
+  // 16-lane groups fill their lanes (C3's 1.1 KB entries: dense 0.525 vs 0.496 ms; profiles/r06h)
+  if (mk && avg > 128 && avg <= 512 && !LSMGPU_KNOB(p.wj, 0u) && !LSMGPU_KNOB(p.weo, 0u) &&
+      LSMGPU_KNOB(p.wdense, 1u)) {
+    copy_entries_dense<COH>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view,
+                            lane, pre, mk);
+    return;
+  }
   // (round 4: each lane's first piece of every entry of a pass loaded before any store left
   // the copy unchanged, 0.6038 vs 0.6042 ms, profiles/r04c; compiled into this kernel it also
   // raised the VGPRs from 44 to 90, 8 -> 5 waves per SIMD: removed)
@@ -1709,9 +1782,10 @@ __global__ void __launch_bounds__(256) wsc_copy_kernel(DecodeParams p) {
   const uint32_t n = uniform(d0.x), K = uniform(d0.y), V = uniform(d0.z), sw = uniform(d0.w);
   const uint64_t en = uniform(d1.x), ek = uniform(d1.y), ev = uniform(d1.z);
   const uint32_t off = uniform(d1.w);
-  __shared__ uint32_t s_chunk[4][kChunkLds];  // copy_chunks' per-wave tables
+  __shared__ uint32_t s_chunk[4][kChunkLds];  // copy_chunks' per-wave tables (diag)
+  __shared__ uint8_t s_mk[4][kWave];           // copy_entries_dense's owner marks
   copy_block(p, b, meta, pre, n, K, V, sw, en, ek, ev, off, sub, split, lane, GlobalBytes{p.data + off},
-             s_chunk[threadIdx.x >> 6], false);
+             s_chunk[threadIdx.x >> 6], false, s_mk[threadIdx.x >> 6]);
 }
 
 

@@ -88,6 +88,7 @@ struct DecodeParams {
   // the tiles copy blocks as soon as their tile's descriptors are published (wncop of them)
   uint32_t wcopyfuse;
   uint32_t wncop;
+  uint32_t wdense;          // (diag) copy: dense piece mapping for blocks of > 128-B entries (1)
 
 };
 
