@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <thread>
 
@@ -161,13 +162,34 @@ class Stager {
   int next_ = 0;
 };
 
-// Copy-pool size: LSMGPU_COPY_THREADS, else half the machine's hardware threads, at most 16
-// (C2 1 GiB from pageable memory, materialize: 8 threads 0.035 s, 16 threads 0.026 s against a
-// 0.0186 s PCIe bound; profiles/r06b)
+// The process's CPU quota (cgroup v2 cpu.max, or v1 cfs quota / period), 0 if none
+inline unsigned cgroup_cpus() {
+  long long q = -1, per = 0;
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char a[32] = {0};
+    if (fscanf(f, "%31s %lld", a, &per) == 2 && a[0] != 'm') q = atoll(a);
+    fclose(f);
+  } else if (FILE* f1 = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+    if (fscanf(f1, "%lld", &q) != 1) q = -1;
+    fclose(f1);
+    if (FILE* f2 = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+      if (fscanf(f2, "%lld", &per) != 1) per = 0;
+      fclose(f2);
+    }
+  }
+  return q > 0 && per > 0 ? (unsigned)std::max(1ll, q / per) : 0u;
+}
+
+// Copy-pool size: LSMGPU_COPY_THREADS, else half the hardware threads, at most 16, and at most
+// one less than the CPU quota (the calling thread memcpys too).  C2 1 GiB from pageable memory,
+// materialize: 8 threads 0.035 s, 16 threads 0.026 s against a 0.0186 s PCIe bound (profiles/r06b)
+// -- on a box whose job quota is 16 CPUs, so the 16 threads of the default then oversubscribed it.
 inline unsigned copy_threads() {
   if (const char* e = getenv("LSMGPU_COPY_THREADS")) return (unsigned)std::max(1, atoi(e));
   const unsigned hw = std::thread::hardware_concurrency();
-  return std::max(1u, std::min(16u, hw / 2));
+  unsigned n = std::max(1u, std::min(16u, hw / 2));
+  if (const unsigned q = cgroup_cpus()) n = std::max(1u, std::min(n, q > 1 ? q - 1 : 1u));
+  return n;
 }
 
 }  // namespace lsmgpu

@@ -10,8 +10,8 @@ for r in 1 2; do
 for c in $CFGS; do
 for v in $VARS; do
   if [ "$v" = "cur" ]; then unset LSMGPU_LIB_VARIANT; else export LSMGPU_LIB_VARIANT=$v; fi
-  timeout -k 10 300 python bench.py --config $c --no-cpu --no-peaks --no-view --steps 20 "$@" > $O/c${c}_${v}_r$r.json 2>> $O/bench.err || { echo "bench failed: c$c $v"; exit 1; }
-  python -c "import json;d=json.loads(open('$O/c${c}_${v}_r$r.json').read().strip().splitlines()[-1]);k=d['roofline']['kernels'];print('C$c $v r$r', d['ms_per_step'], d['value'], k['walk_ms'], k['copy_ms'], d['encode']['kernel_ms'], d['parity'][:13])"
+  timeout -k 10 300 python bench.py --config $c --no-cpu --no-peaks ${NOVIEW---no-view} --steps 20 "$@" > $O/c${c}_${v}_r$r.json 2>> $O/bench.err || { echo "bench failed: c$c $v"; exit 1; }
+  python -c "import json;d=json.loads(open('$O/c${c}_${v}_r$r.json').read().strip().splitlines()[-1]);k=d['roofline']['kernels'];print('C$c $v r$r', d['ms_per_step'], d['value'], k['walk_ms'], k['copy_ms'], d['encode']['kernel_ms'], (d.get('view_mode') or {}).get('kernel_ms'), d['parity'][:13])"
 done
 done
 done
