@@ -144,7 +144,8 @@ int lsmgpu_decode_blocks(lsmgpu_ctx* ctx, const uint8_t* data, uint64_t data_len
  * through page-locked buffers the ctx owns, filled and drained by memcpy on a small per-ctx
  * thread pool (LSMGPU_COPY_THREADS, default half the hardware threads, at most 16).  So a caller that wants
  * one copy of a table end to end reads the file into lsmgpu_host_alloc memory.
- * Every host call has finished all DMA into or out of caller memory when it returns. */
+ * Every host call has finished all DMA into or out of caller memory when it returns.  A device
+ * pointer passed as host `data` (data_on_device = 0) is LSMGPU_ERR_ARG. */
 int lsmgpu_host_alloc(lsmgpu_ctx* ctx, uint64_t bytes, void** out);  /* hipHostMalloc, portable */
 int lsmgpu_host_free(lsmgpu_ctx* ctx, void* p);  /* p NULL: no-op; ctx may be NULL (any device) */
 

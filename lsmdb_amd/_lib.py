@@ -11,7 +11,7 @@ from ctypes import POINTER, c_int, c_int32, c_int64, c_uint8, c_uint32, c_uint64
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liblsmgpu.so")
-# diagnostics only: an alternate in-tree build (e.g. liblsmgpu_stamps.so, LSMGPU_BUILD_STAMPS=1)
+# diagnostics only: an alternate in-tree build (e.g. liblsmgpu_diag.so, LSMGPU_BUILD_DIAG=1)
 if os.environ.get("LSMGPU_LIB_VARIANT"):
     LIB_PATH = os.path.join(_HERE, f"liblsmgpu_{os.environ['LSMGPU_LIB_VARIANT']}.so")
 

@@ -784,6 +784,7 @@ int lsmgpu_decode_blocks(lsmgpu_ctx* c, const uint8_t* data, uint64_t data_len,
   if (data_len > 0xffffffffull) return LSMGPU_ERR_TOO_LARGE;
   if (mode & ~(LSMGPU_MODE_MATERIALIZE | LSMGPU_MODE_VIEW)) return LSMGPU_ERR_ARG;
   HIPC(hipSetDevice(c->device));
+  if (!data_on_device && data_len && device_memory(data)) return LSMGPU_ERR_ARG;  // (flag mismatch)
   uint32_t max_len = 0;
   for (uint64_t b = 0; b < nblk; b++) max_len = std::max(max_len, blk_len[b]);
   const bool query0 = !out->key_data && !out->key_end && !out->val_data && !out->val_end &&

@@ -559,7 +559,7 @@ __global__ void __launch_bounds__(64) decode_kernel(DecodeParams p) {
     ring_len = b < nblk ? p.blk_len[b] : 0u;
   };
 #ifdef LSMGPU_STAMPS
-  // diagnostic build only (LSMGPU_BUILD_STAMPS=1): per-phase s_memtime totals
+  // diagnostic build only (LSMGPU_BUILD_DIAG=1): per-phase s_memtime totals
   const bool st = p.stamps != nullptr;
   uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tprev = st ? stamp() : 0;

@@ -440,7 +440,7 @@ __device__ __forceinline__ void fused_copier(const DecodeParams& p, uint32_t c, 
 // 266,403 blocks: 1,041 tiles of 256 for 1,024 resident slots, and the 17-tile second wave cost
 // the walk 0.030 ms and the view decode 0.045 ms (same-box A/B, profiles/r05c); 463 tiles of 576
 // are all resident.  WIDE keeps no per-lane tables besides the rows (no s_first / s_off).
-// Diagnostic build only (LSMGPU_BUILD_STAMPS=1, run with LSMGPU_STAMPS=1): per tile, the
+// Diagnostic build only (LSMGPU_BUILD_DIAG=1, run with LSMGPU_STAMPS=1): per tile, the
 // s_memrealtime (100 MHz) of its start, its walk's end (every wave), its look-back's end and its
 // epilogue's end (wave 0), written to p.stamps[16 + 4 tile ..] and summarized by the host.
 #ifdef LSMGPU_STAMPS

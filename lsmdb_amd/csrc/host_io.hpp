@@ -65,6 +65,18 @@ inline bool runtime_pinned(const void* p, uint64_t n) {
   return true;
 }
 
+// Whether p is device memory (a data_on_device = 0 call handed a device pointer: staging it with
+// memcpy would fault on the host)
+inline bool device_memory(const void* p) {
+  hipPointerAttribute_t a{};
+  const hipError_t e = hipPointerGetAttributes(&a, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice;
+}
+
 // The staging pair of one context: two page-locked pieces used alternately, each guarded by an
 // event on the stream of the DMA that last used it, so host memcpy of one piece overlaps the
 // DMA of the other.

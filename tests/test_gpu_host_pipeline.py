@@ -264,3 +264,20 @@ def test_host_pipeline_fallbacks(codec, oracle, monkeypatch):
     ref = oracle.decode(full, o3, l3)
     assert ref.key_data.size > len(full)
     _assert_same(codec.decode_host(full, o3, l3), ref, "expanding keys")
+
+
+def test_host_mode_rejects_device_pointer(codec, oracle):
+    """data_on_device = 0 with a device pointer is an argument error (LSMGPU_ERR_ARG), not a host
+    memcpy from device memory."""
+    import torch
+    c2 = _cols(2, 5000, seed=81)
+    body, _, _ = oracle.build_cols(c2.keys, c2.key_end, c2.vs, c2.vs_end, 0, 4096)
+    sst = body + b"{}" + (2).to_bytes(4, "big")
+    off, ln, _, _ = oracle.parse_index(sst)
+    d_sst = torch.from_numpy(np.frombuffer(sst, np.uint8).copy()).cuda()
+    d = _lib.LsmgpuDecoded()
+    bf = np.zeros(off.size + 1, np.uint32)
+    d.blk_first = _ptr(bf)
+    rc = _lib.lib().lsmgpu_decode_blocks(codec._ctx, d_sst.data_ptr(), len(sst), 0, _ptr(off), _ptr(ln),
+                                         off.size, MODE_VIEW, byref(d))
+    assert rc == _lib.ERR_ARG
