@@ -929,6 +929,7 @@ int lsmgpu_encode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_keys, const uint3
   p.out = d_out;
   p.data_len = data_len;
   p.flags = d_flags;
+  p.pad = c->flags.as<uint8_t>() + 128;  // 16 readable bytes (encode_pipe_kernel)
   HIPC(launch_encode(p, c->num_cus, c->stream));
   return LSMGPU_OK;
 }
@@ -1296,6 +1297,7 @@ int encode_tables_impl(lsmgpu_ctx* c, const uint8_t* d_keys, const uint32_t* d_k
   p.tbl_blk = d_tbl_blk;
   p.tbl_out = d_tbl_out;
   p.ntables = tables_cap;  // the kernel reads the real count from the arrays' closing entries
+  p.pad = c->flags.as<uint8_t>() + 128;  // 16 readable bytes (encode_pipe_kernel)
   HIPC(launch_encode(p, c->num_cus, c->stream));
   return LSMGPU_OK;
 }

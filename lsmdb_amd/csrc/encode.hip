@@ -6,10 +6,13 @@
 // (each earlier entry contributes its 10-B header, its full key -- keyDiff always returns the
 // whole key, builder.go:74-82 -- and its ValueStruct bytes; each earlier block its 13-B
 // terminator, builder.go:121-123).  One wave per block; groups of J lanes take one entry each:
-// lane 0 of the group writes the synthesised header (8-B + 2-B stores), and the J lanes copy
-// the key and the vs-enc bytes global -> global as unaligned 16-B pieces (the last piece
-// overlapping back inside its stream, two overlapping 8/4-B pieces or single bytes below
-// 16 B), so no store crosses into a neighbour's bytes.  J follows the average entry size.
+// lane 0 of the group writes the synthesised header (with the key's first 6 bytes, one 16-B
+// store), and the J lanes copy the key and the vs-enc bytes global -> global as unaligned 16-B
+// pieces (the last piece overlapping back inside its stream, two overlapping 8/4-B pieces or
+// single bytes below 16 B), so no store crosses into a neighbour's bytes.  J follows the
+// average entry size.  The product kernel is encode_pipe_kernel (each lane's first piece of the
+// next entry pass loaded before this pass's stores); encode_kernel, the unpipelined order with
+// G groups per trip, is kept for the diagnostic build's A/Bs.
 #include <cstdlib>
 
 #include "codec_common.hpp"
@@ -53,19 +56,27 @@ __device__ __forceinline__ void store_header(uint8_t* d, uint32_t klen, uint32_t
   __builtin_memcpy(d + 8, &lo, 2);
 }
 
-template <uint32_t J, uint32_t G>
-__global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
-  constexpr uint32_t EPP = kWave / J;      // entries per group pass; G group passes per loop
-                                           // trip, every offset load issued first
-  const uint32_t lane = lane_id();
-  const uint32_t b = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
-  // table context: output image, its data length, block count, and the entry / key / vs bases
-  // positions are relative to (one table, or table t of a compaction's output in tbl_* mode)
+// One output block's table context: its entries [f, l), the output image, the image's data
+// length and block count, and the entry / key / vs bases positions are relative to (one table,
+// or table t of a compaction's output in tbl_* mode).  False: past the last block, or a block of
+// no entries (its terminator written here).
+struct EncBlock {
+  uint64_t f, l, e0b, kb0, vb0, dl;
+  uint32_t lb, tnb;
+  uint8_t* out;
+  // entry e's position in its table: 10 (e - e0b) + key bytes + vs bytes before it + 13 per block
+  __device__ __forceinline__ uint32_t position(uint64_t e, uint64_t ks, uint64_t vs0) const {
+    return (uint32_t)(10 * (e - e0b) + (ks - kb0) + (vs0 - vb0)) + 13u * lb;
+  }
+};
+
+__device__ __forceinline__ bool enc_block(const EncodeParams& p, uint32_t b, uint32_t lane,
+                                          EncBlock& k) {
   uint64_t f, l, e0b = 0, kb0 = 0, vb0 = 0, dl = p.data_len;
   uint32_t lb = b, tnb = p.nblocks;
   uint8_t* out = p.out;
   if (p.tbl_first) {
-    if (b >= p.tbl_blk[p.ntables]) return;
+    if (b >= p.tbl_blk[p.ntables]) return false;
     uint32_t lo = 0, hi = p.ntables - 1;  // table of block b: largest t with tbl_blk[t] <= b
     while (lo < hi) {
       const uint32_t mid = (lo + hi + 1) >> 1;
@@ -83,36 +94,47 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
     out = p.out + p.tbl_out[t];
     dl = 10 * (ee - e0b) + (key_start(p, ee) - kb0) + (vs_start(p, ee) - vb0) + 13ull * tnb;
   } else {
-    if (b >= p.nblocks) return;
+    if (b >= p.nblocks) return false;
     block_range(p, b, f, l);
   }
-  f = uniform64(f);
-  l = uniform64(l);
-  e0b = uniform64(e0b);
-  kb0 = uniform64(kb0);
-  vb0 = uniform64(vb0);
-  dl = uniform64(dl);
-  const uint64_t m = l - f;
-  const uint32_t blk13 = 13u * lb;
-  // entry e's position in its table: 10 (e - e0b) + key bytes + vs bytes before it + 13 per block
-  auto position = [&](uint64_t e, uint64_t ks, uint64_t vs0) -> uint32_t {
-    return (uint32_t)(10 * (e - e0b) + (ks - kb0) + (vs0 - vb0)) + blk13;
-  };
-
-  if (m == 0) {  // a block of no entries: the terminator alone (table_test.go:514)
+  k.f = uniform64(f);
+  k.l = uniform64(l);
+  k.e0b = uniform64(e0b);
+  k.kb0 = uniform64(kb0);
+  k.vb0 = uniform64(vb0);
+  k.dl = uniform64(dl);
+  k.lb = lb;
+  k.tnb = tnb;
+  k.out = out;
+  if (k.l == k.f) {  // a block of no entries: the terminator alone (table_test.go:514)
     if (lane == 0) {
-      const uint32_t bs = position(f, key_start(p, f), vs_start(p, f));
+      const uint32_t bs = k.position(k.f, key_start(p, k.f), vs_start(p, k.f));
       uint8_t* t = out + bs;
       store_header(t, 0, 3, 0xffffffffu);
       t[10] = 0;
       t[11] = 0;
       t[12] = 0;
-      store_be32(out + dl + 4ull * lb, bs + 13);
+      store_be32(out + k.dl + 4ull * lb, bs + 13);
     }
-    if (lane == 1 && lb == tnb - 1) store_be32(out + dl + 4ull * tnb, tnb);
-    return;
+    if (lane == 1 && lb == tnb - 1) store_be32(out + k.dl + 4ull * tnb, tnb);
+    return false;
   }
-  if (lane == 1 && lb == tnb - 1) store_be32(out + dl + 4ull * tnb, tnb);
+  if (lane == 1 && lb == tnb - 1) store_be32(out + k.dl + 4ull * tnb, tnb);
+  return true;
+}
+
+template <uint32_t J, uint32_t G>
+__global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
+  constexpr uint32_t EPP = kWave / J;      // entries per group pass; G group passes per loop
+                                           // trip, every offset load issued first
+  const uint32_t lane = lane_id();
+  const uint32_t b = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+  EncBlock k;
+  if (!enc_block(p, b, lane, k)) return;
+  const uint64_t f = k.f, m = k.l - k.f, dl = k.dl;
+  const uint32_t lb = k.lb;
+  uint8_t* const out = k.out;
+  auto position = [&](uint64_t e, uint64_t ks, uint64_t vs0) { return k.position(e, ks, vs0); };
 
   // Absolute entry positions are closed-form (no block base needed to place bytes); the block
   // start is entry f's position (lane 0, first pass), a header's prev is the previous entry's
@@ -225,6 +247,189 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
   if (bad) atomicOr(p.flags, bad);
 }
 
+// encode_pipe_kernel<J, U2> (the product encoder): encode_kernel<J, 1> with each lane's first
+// 16-B piece of the next entry pass loaded before this pass's stores.  The compiled
+// encode_kernel issues every piece as load -> s_waitcnt vmcnt(0) -> store, and the header's 8-B
+// key read the same way; on gfx950 vmcnt counts stores as well as loads, so each wait also drains
+// the pass's earlier stores, and a pass costs load and store round trips back to back.  Here:
+//  * the header's key bytes come from the lane's own first piece (key piece 0 whenever the key
+//    is >= 16 B): no separate read;
+//  * the wait for pass i + 1's pieces leaves pass i's stores in flight.  For the compiler to
+//    count those stores they must not sit in a branch: the header and first-piece stores are
+//    buffer stores every lane issues, a lane with nothing to write giving an offset past the
+//    image (the range check drops it).  The offsets come from a window of 64 entries held one
+//    per lane, loaded (and waited for) once per 64 entries, so no other wait stays in the loop;
+//  * U2: two passes per loop trip, each loading into the other's registers (no register copy,
+//    and so no wait, at the back edge), the first pass peeled so that the loop is entered as it
+//    loops.
+// Pieces past a lane's first (entries of more than J pieces) and streams under 16 B keep the
+// plain load -> store order.  Same bytes as encode_kernel.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kNoStore = 0xfffffff0u;    // a buffer offset past any image: the store is dropped
+constexpr int kRsrcWord3 = 0x00020000;        // gfx9 buffer resource word 3 (32-bit data format)
+struct EncPass {
+  uint64_t sk, sv;              // where the key / vs bytes are read
+  uint32_t klen, vlen, pos, kp, np, r;
+  bool on;
+};
+
+template <uint32_t J, bool U2>
+__global__ void __launch_bounds__(256) encode_pipe_kernel(EncodeParams p) {
+  constexpr uint32_t EPP = kWave / J;
+  const uint32_t lane = lane_id();
+  const uint32_t b = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+  EncBlock k;
+  if (!enc_block(p, b, lane, k)) return;
+  const uint64_t f = k.f, m = k.l - k.f, dl = k.dl;
+  const uint32_t lb = k.lb;
+  uint8_t* const out = k.out;
+  const uint32_t j = lane & (J - 1);
+  uint32_t bad = 0, carry = 0, bs = 0;
+  // offsets of a window of 64 entries [w0, w0 + 64) of the block, one entry per lane: its key /
+  // vs start and end, and in gather mode the source starts.  A pass (EPP | 64 entries) lies in
+  // one window; off lanes (past the block's end) read garbage that nothing uses.
+  uint32_t wks, wke, wvs, wve, wsk = 0, wsv = 0;
+  uint64_t w0 = 0;
+  auto window = [&](uint64_t b0) {
+    w0 = b0;
+    const uint64_t r = b0 + lane, e = f + (r < m ? r : m - 1);
+    wks = (uint32_t)key_start(p, e);
+    wvs = (uint32_t)vs_start(p, e);
+    wke = p.key_end[e];
+    wve = p.vs_end[e];
+    if (p.src) {
+      const uint32_t si = p.src[e];
+      wsk = si ? p.src_key_end[si - 1] : 0u;
+      wsv = si ? p.src_vs_end[si - 1] : 0u;
+    }
+    // the window lands here, so no wait for it stays inside the passes (vmcnt counts stores too:
+    // such a wait would drain the previous pass's stores on every trip)
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+  };
+  // the pass over entries [e0, e0 + EPP): offsets by lane shuffle from the window, lengths,
+  // positions, piece counts
+  auto meta = [&](uint64_t e0, EncPass& s) {
+    const uint64_t r = e0 + lane / J;
+    s.r = (uint32_t)r;
+    s.on = r < m;
+    const uint64_t e = f + (s.on ? r : m - 1);
+    const int i = (int)((r - w0) & (kWave - 1));
+    const uint64_t ks = (uint32_t)__shfl((int)wks, i), ke = (uint32_t)__shfl((int)wke, i);
+    const uint64_t vs0 = (uint32_t)__shfl((int)wvs, i), ve = (uint32_t)__shfl((int)wve, i);
+    if (p.src) {
+      s.sk = (uint32_t)__shfl((int)wsk, i);
+      s.sv = (uint32_t)__shfl((int)wsv, i);
+    } else {
+      s.sk = ks;
+      s.sv = vs0;
+    }
+    const uint64_t kl64 = ke - ks, vl64 = ve - vs0;
+    s.klen = (uint32_t)kl64;
+    s.vlen = (uint32_t)vl64;
+    s.pos = k.position(e, ks, vs0);
+    if (s.on && j == 0) {
+      if (kl64 <= 8 || kl64 > 0xffff) bad |= 1;  // ParseKey needs len(key) > 8 (y.go:93-100)
+      if (vl64 > 0xffff) bad |= 2;                // header vlen is a uint16
+    }
+    s.kp = pieces16(s.klen);
+    s.np = s.on ? s.kp + pieces16(s.vlen) : 0u;
+  };
+  // the lane's first piece (q = j) when its stream is >= 16 B: source and destination offsets
+  auto first = [&](const EncPass& s, const uint8_t*& src, uint32_t& dst) -> bool {
+    if (j >= s.np) return false;
+    const bool key = j < s.kp;
+    const uint32_t len = key ? s.klen : s.vlen;
+    if (len < 16) return false;
+    const uint32_t o = min(16 * (key ? j : j - s.kp), len - 16);
+    src = (key ? p.keys + s.sk : p.vs + s.sv) + o;
+    dst = s.pos + 10 + (key ? 0u : s.klen) + o;
+    return true;
+  };
+
+  // The header and first-piece stores go out as buffer stores over the table image, issued by
+  // every lane (a lane with nothing to write gives an offset past the image's end, and the
+  // hardware's range check drops it): with no branch around them the compiler counts them, so the
+  // wait for the next pass's first pieces leaves them in flight (a store in a branch counts as
+  // possibly absent, and the wait then drains it).  Offsets are 32-bit: an image is < 4 GiB.
+  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>(uniform64(reinterpret_cast<uint64_t>(out))), 0,
+      (int)(uint32_t)(dl < kNoStore ? dl : kNoStore), kRsrcWord3);
+  auto put16 = [&](const u32x4& v, uint32_t o) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, orsrc, o, 0, 0);
+  };
+  // one pass: the next pass's offsets and first pieces into (nx, nv, n16, nd) -- loaded before
+  // any store of this one, unconditionally (from p.pad when the lane has no such piece) -- then
+  // this pass's header, terminator and pieces from (cu, av, a16, ad)
+  auto step = [&](const EncPass& cu, const uint4& av, bool a16, uint32_t ad, uint64_t e0,
+                  EncPass& nx, uint4& nv, bool& n16, uint32_t& nd) {
+    if (((e0 + EPP) & (kWave - 1)) == 0 && e0 + EPP < m) window(e0 + EPP);  // (uniform)
+    meta(e0 + EPP, nx);  // past the block's end: every entry off, no pieces
+    const uint8_t* nsrc = p.pad;
+    n16 = first(nx, nsrc, nd);
+    __builtin_memcpy(&nv, nsrc, 16);
+    // headers (prev = the lane group below, else the previous pass)
+    const uint32_t below = __shfl_up(cu.pos, J);
+    const uint32_t prev = cu.r == 0 ? 0xffffffffu : (lane < J ? carry : below) - bs;  // builder.go:95-99
+    // header + the key's first 6 bytes as one 16-B store, the key bytes from this lane's first
+    // piece (key piece 0: the key is >= 16 B); shorter keys: 8-B + 2-B header stores
+    const u32x4 w = {bswap16(cu.klen) << 16,                                // plen 00 00 | klen BE
+                     bswap16(cu.vlen) | (bswap16(prev >> 16) << 16),       // vlen BE | prev[31:16] BE
+                     bswap16(prev & 0xffffu) | (av.x << 16),               // prev[15:0] BE | key[0..1]
+                     (av.x >> 16) | (av.y << 16)};                         // key[2..5]
+    const bool hdr = cu.on && j == 0;
+    put16(w, hdr && a16 ? cu.pos : kNoStore);
+    if (hdr && !a16) store_header(out + cu.pos, cu.klen, cu.vlen, prev);
+    if (cu.on && j == 1 && cu.r == m - 1) {  // terminator + restart (builder.go:121-123,146-160)
+      const uint32_t te = cu.pos + 10 + cu.klen + cu.vlen;
+      uint8_t* t = out + te;
+      store_header(t, 0, 3, cu.pos - bs);
+      t[10] = 0;
+      t[11] = 0;
+      t[12] = 0;
+      store_be32(out + dl + 4ull * lb, te + 13);
+    }
+    carry = readlane(cu.pos, kWave - J);
+    // pieces: the preloaded first one, then the rest in load -> store order
+    put16(u32x4{av.x, av.y, av.z, av.w}, a16 ? ad : kNoStore);
+    for (uint32_t q = a16 ? j + J : j; q < cu.np; q += J) {
+      const bool key = q < cu.kp;
+      copy_piece16(out + cu.pos + 10 + (key ? 0u : cu.klen), key ? p.keys + cu.sk : p.vs + cu.sv,
+                   key ? cu.klen : cu.vlen, key ? q : q - cu.kp);
+    }
+  };
+  EncPass pa, pb;
+  uint4 va, vb;
+  bool fa, fb;
+  uint32_t da = 0, db = 0;
+  window(0);
+  meta(0, pa);
+  bs = readlane(pa.pos, 0);
+  const uint8_t* src0 = p.pad;
+  fa = first(pa, src0, da);
+  __builtin_memcpy(&va, src0, 16);
+  if (U2) {
+    // two passes per trip, each loading into the other's registers: no register copy (and so no
+    // wait for the loads in flight) at the loop's back edge
+    // (the first pass peeled: the loop is then entered, as it loops, with the previous pass's two
+    // buffer stores issued after the pending pieces, so one wait count serves both entries)
+    step(pa, va, fa, da, 0, pb, vb, fb, db);
+    for (uint64_t e0 = EPP; e0 < m; e0 += 2 * EPP) {
+      step(pb, vb, fb, db, e0, pa, va, fa, da);
+      if (e0 + EPP >= m) break;
+      step(pa, va, fa, da, e0 + EPP, pb, vb, fb, db);
+    }
+  } else {
+    for (uint64_t e0 = 0; e0 < m; e0 += EPP) {
+      step(pa, va, fa, da, e0, pb, vb, fb, db);
+      pa = pb;
+      va = vb;
+      fa = fb;
+      da = db;
+    }
+  }
+  if (bad) atomicOr(p.flags, bad);
+}
+
 // Builder.ReachedCapacity (builder.go:140-143) as compactBuildTables applies it before every
 // Add (levels.go:265-271): a table holding e entries [s, s + e) is closed when
 //   10e + K + V + 13 fb + 8 + 4 fb + 8 > cap,   fb = (e - 1) / epb finished blocks
@@ -314,7 +519,19 @@ hipError_t launch_cut_tables(const CutParams& p, hipStream_t s) {
 template <uint32_t J, uint32_t G>
 static hipError_t launch_enc(const EncodeParams& p, hipStream_t s) {
   // tbl_* mode: p.nblocks is an upper bound on the blocks of all tables (grid size)
-  hipLaunchKernelGGL((encode_kernel<J, G>), dim3((p.nblocks + 3) / 4), dim3(256), 0, s, p);
+#ifdef LSMGPU_DIAG
+  if (G > 1 || !p.pipe) {  // encode_kernel: G entry groups per trip, or the unpipelined order
+    hipLaunchKernelGGL((encode_kernel<J, G>), dim3((p.nblocks + 3) / 4), dim3(256), 0, s, p);
+    return hipGetLastError();
+  }
+#endif
+#ifdef LSMGPU_DIAG
+  if (p.pipe == 1) {  // one pass per loop trip (register copies at the back edge)
+    hipLaunchKernelGGL((encode_pipe_kernel<J, false>), dim3((p.nblocks + 3) / 4), dim3(256), 0, s, p);
+    return hipGetLastError();
+  }
+#endif
+  hipLaunchKernelGGL((encode_pipe_kernel<J, true>), dim3((p.nblocks + 3) / 4), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
@@ -324,6 +541,10 @@ hipError_t launch_encode(const EncodeParams& p0, int num_cus, hipStream_t s) {
   // one 16-B store for the header and the key's first 6 bytes (same box, C2 encode 0.5864-0.5895
   // -> 0.5627-0.5667 ms, profiles/r05ae); diag build: LSMGPU_ENC_HDR16=0 keeps the 8-B + 2-B stores
   p.hdr16 = 1u;
+  // encode_pipe_kernel, two passes per trip: same box, C2 encode 0.565-0.566 -> 0.480-0.481 ms,
+  // C5 0.760-0.762 -> 0.558-0.560 ms, C3 0.545-0.549 -> 0.441-0.447 ms (profiles/r06o); diag
+  // build: LSMGPU_ENC_PIPE=0 keeps encode_kernel, 1 the one-pass-per-trip loop
+  p.pipe = 2u;
   // J = lanes per entry ~ the average entry's 16-B pieces (C2: 129 B -> 8; C3: ~1.1 KB -> 64)
   const uint64_t avg = p.n ? (p.key_total + p.vs_total) / p.n : 120;
   // LSMGPU_ENC_J (test hook): one of the compiled J (4, 8, 16) whatever the entry size
@@ -335,6 +556,7 @@ hipError_t launch_encode(const EncodeParams& p0, int num_cus, hipStream_t s) {
   }
 #ifdef LSMGPU_DIAG
   if (const char* h16 = getenv("LSMGPU_ENC_HDR16")) p.hdr16 = atoi(h16) == 0 ? 0u : 1u;
+  if (const char* pe = getenv("LSMGPU_ENC_PIPE")) p.pipe = (uint32_t)atoi(pe);  // 0, 1, 2 (unrolled)
   const char* ge = getenv("LSMGPU_ENC_G");  // A/B: entry-group passes per loop trip
   const int g = ge ? atoi(ge) : 1;           // measured: C2 G=1 0.61 ms, 2 0.68, 4 0.72
   if (g == 4) return avg <= 128 ? launch_enc<8, 4>(p, s) : launch_enc<16, 4>(p, s);

@@ -499,10 +499,13 @@ def test_wsc_many_tiles(codec, oracle, monkeypatch, chunk, lookback):
                                                [("LSMGPU_ENC_G", "2"), ("LSMGPU_ENC_G", "4"),
                                                 ("LSMGPU_ENC_HDR16", "1"), ("LSMGPU_ENC_HDR16", "0")]))
 def test_encode_template_instances(codec, oracle, monkeypatch, knob, val):
-    """Every encode_kernel<J, G> instance the A/B knobs select (LSMGPU_ENC_J / LSMGPU_ENC_G)
+    """Every encode kernel instance the knobs select (LSMGPU_ENC_J: encode_pipe_kernel<J>; diag
+    build: encode_kernel<J, G> with LSMGPU_ENC_G, its header stores with LSMGPU_ENC_HDR16)
     changes which passes take the lane-shuffle offset path (advisor, round 1): each is checked
     bit-exact against the oracle Builder on C1 / C2 / C5 and 100 / 180 entries per block."""
     monkeypatch.setenv(knob, val)
+    if knob == "LSMGPU_ENC_HDR16":  # encode_kernel's header stores (encode_pipe_kernel has its own)
+        monkeypatch.setenv("LSMGPU_ENC_PIPE", "0")
     for cfg, n, epb in [(1, 10000, None), (2, 20000, None), (5, 20000, None), (2, 20000, 100),
                         (2, 20000, 180)]:
         c = _cols(cfg, n, seed=n + 1)
@@ -512,6 +515,33 @@ def test_encode_template_instances(codec, oracle, monkeypatch, knob, val):
         out, dl, rs = codec.encode_host(c.keys, c.key_end, c.vs, c.vs_end, e, bb)
         assert dl == ref_dl and np.array_equal(rs, ref_rs)
         assert out == ref, f"{knob}={val} cfg={cfg} epb={epb}"
+
+
+@pytest.mark.skipif(not DIAG, reason="LSMGPU_ENC_PIPE: diagnostic build only")
+@pytest.mark.parametrize("pipe", ["1", "2"])
+@pytest.mark.parametrize("j", ["4", "8", "16"])
+def test_encode_pipe_kernel(codec, oracle, monkeypatch, j, pipe):
+    """encode_pipe_kernel<J> (the next pass's first pieces loaded before this pass's stores, the
+    header's key bytes from the lane's own first piece) bit-exact against the oracle Builder:
+    C1 / C2 / C5, 100 / 180 entries per block (offset loads past the first 64 entries), and
+    random short keys and values (9-40 B keys, 3-60 B vs: streams under 16 B); LSMGPU_ENC_PIPE=2:
+    two passes per loop trip (no register copies at the back edge)."""
+    monkeypatch.setenv("LSMGPU_ENC_PIPE", pipe)
+    monkeypatch.setenv("LSMGPU_ENC_J", j)
+    cases = []
+    for cfg, n, epb in [(1, 10000, None), (2, 20000, None), (5, 20000, None), (2, 20000, 100),
+                        (2, 20000, 180)]:
+        c = _cols(cfg, n, seed=n + 3)
+        cases.append(((c.keys, c.key_end, c.vs, c.vs_end),
+                      c.entries_per_block if epb is None else epb,
+                      c.block_bytes if epb is None else 0))
+    cases.append((_random_cols(20000, 29), 0, 4096))
+    cases.append((_random_cols(20000, 31), 70, 0))
+    for cols, e, bb in cases:
+        ref, ref_dl, ref_rs = oracle.build_cols(*cols, e, bb)
+        out, dl, rs = codec.encode_host(*cols, e, bb)
+        assert dl == ref_dl and np.array_equal(rs, ref_rs)
+        assert out == ref, f"J={j} epb={e} bb={bb}"
 
 
 @pytest.mark.skipif(not DIAG, reason="LSMGPU_WSC_J: diagnostic build only")
