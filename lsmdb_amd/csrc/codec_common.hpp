@@ -106,6 +106,19 @@ __device__ __forceinline__ int compare_keys(const uint8_t* a, uint32_t la, const
   return c ? c : bytes_compare(a + la - 8, 8, b + lb - 8, 8);
 }
 
+// Range-checked buffer accesses (raw buffer loads / stores over a resource of `bytes` bytes at a
+// wave-uniform base): an offset at or past the end reads zeros and drops the store without a
+// memory access, so every lane can issue the instruction and none needs a branch around it.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+constexpr uint32_t kNoStore = 0xfffffff0u;  // an offset past any resource (resources are < 4 GiB - 16)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base, uint64_t bytes) {
+  // word 3: gfx9 32-bit data format, the range check on raw offsets
+  return __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>(uniform64(reinterpret_cast<uint64_t>(base))), 0,
+      (int)(uint32_t)(bytes < kNoStore ? bytes : kNoStore), 0x00020000);
+}
+
 // A stream of `len` bytes copied global -> global (any alignment) as independent pieces:
 // 16-B pieces, the last one overlapping back inside the stream; below 16 B two overlapping
 // 8-B or 4-B pieces; below 4 B single bytes.  No piece touches a byte outside the stream, so

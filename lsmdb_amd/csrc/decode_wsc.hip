@@ -1666,6 +1666,108 @@ __device__ __forceinline__ void copy_entries_dense(const DecodeParams& p, const 
   }
 }
 
+// The entries of a block of < 64 entries with no prefix-compressed entry, PIPELINED (materialize
+// without view; the encoder's scheme, encode.hip encode_pipe_kernel): J lanes per entry, entry
+// groups g = 0, 1, ... of 64 / J entries, records from `pre` by lane shuffle.  Each lane's first
+// piece of group g + 1 is loaded before group g's stores, and every load and store of the
+// pipeline is a range-checked buffer access all lanes issue (a lane with nothing to move gives
+// an offset past the resource: zeros read, store dropped), so the compiler's wait for group
+// g + 1's pieces counts group g's stores and leaves them in flight -- the plain copy waits
+// (vmcnt counts stores too) for every earlier store before each piece.  In the pipeline: 16-B
+// pieces of either stream and 8-B value pieces (a 15-B value pointer's); the other pieces (key
+// streams under 16 B, value streams under 8 B, pieces past a lane's first) follow it in the
+// plain order.  key_end / val_end: one lane per entry, two buffer stores, after group 0's loads.
+template <uint32_t J>
+__device__ __forceinline__ void copy_entries_pipe(const DecodeParams& p, const uint8_t* blk,
+                                                  uint8_t* kbase, uint8_t* vbase, uint32_t n,
+                                                  uint32_t K, uint32_t V, uint64_t en, uint64_t ek,
+                                                  uint64_t ev, uint32_t off, uint32_t lane,
+                                                  uint32_t pre) {
+  constexpr uint32_t EPP = kWave / J;
+  const uint32_t j = lane & (J - 1);
+  const __amdgpu_buffer_rsrc_t in = buffer_rsrc(blk, p.data_len - off);
+  const __amdgpu_buffer_rsrc_t kr = buffer_rsrc(kbase, kbase ? K : 0u);
+  const __amdgpu_buffer_rsrc_t vr = buffer_rsrc(vbase, vbase ? V : 0u);
+  // group g's pipelined piece of this lane: input offset (kNoStore: none) and destinations
+  struct Pc {
+    uint32_t src, k16, v16, v8;
+  };
+  auto fields = [&](uint32_t e, uint32_t& hp, uint32_t& kl, uint32_t& vl, uint32_t& ko, uint32_t& vo) {
+    const uint32_t ec = min(e, n - 1);
+    const uint32_t m0 = (uint32_t)__shfl((int)pre, (int)ec), m1 = (uint32_t)__shfl((int)pre, (int)ec + 1);
+    hp = m0 & 0xffffu;
+    vo = m0 >> 16;
+    vl = (m1 >> 16) - vo;
+    kl = (m1 & 0xffffu) - hp - 10 - vl;  // stored key bytes
+    ko = hp - 10 * ec - vo;              // (no prefix-compressed entry here)
+  };
+  auto piece = [&](uint32_t g) -> Pc {
+    const uint32_t e = g * EPP + lane / J;
+    uint32_t hp, kl, vl, ko, vo;
+    fields(e, hp, kl, vl, ko, vo);
+    const uint32_t kp = pieces16(kl), np = kp + pieces16(vl);
+    Pc c{kNoStore, kNoStore, kNoStore, kNoStore};
+    if (e < n && j < np) {
+      if (j < kp) {
+        if (kl >= 16) {
+          const uint32_t o = min(16 * j, kl - 16);
+          c.src = hp + 10 + o;
+          c.k16 = ko + o;
+        }
+      } else if (vl >= 8) {
+        const uint32_t q = j - kp, o = vl >= 16 ? min(16 * q, vl - 16) : (q ? vl - 8 : 0u);
+        c.src = hp + 10 + kl + o;
+        if (vl >= 16) c.v16 = vo + o;
+        else c.v8 = vo + o;
+      }
+    }
+    return c;
+  };
+  auto load = [&](const Pc& c) -> u32x4 { return __builtin_amdgcn_raw_buffer_load_b128(in, c.src, 0, 0); };
+  auto store = [&](const Pc& c, const u32x4& v) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, kr, c.k16, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(v, vr, c.v16, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, vr, c.v8, 0, 0);
+  };
+  const uint32_t ng = (n + EPP - 1) / EPP;
+  Pc ca = piece(0);
+  u32x4 va = load(ca);
+  {  // key_end / val_end of every entry (lane = entry)
+    uint32_t hp, kl, vl, ko, vo;
+    fields(lane, hp, kl, vl, ko, vo);
+    const bool on = lane < n;
+    const __amdgpu_buffer_rsrc_t ke = buffer_rsrc(p.key_end ? p.key_end + en : nullptr, p.key_end ? 4ull * n : 0ull);
+    const __amdgpu_buffer_rsrc_t ve = buffer_rsrc(p.val_end ? p.val_end + en : nullptr, p.val_end ? 4ull * n : 0ull);
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(ek + ko + kl), ke, on ? 4 * lane : kNoStore, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(ev + vo + vl), ve, on ? 4 * lane : kNoStore, 0, 0);
+  }
+  for (uint32_t g = 0; g < ng; g += 2) {  // two groups per trip: no register copy at the back edge
+    const Pc cb = piece(g + 1);  // (past the last group: every lane off, nothing read)
+    const u32x4 vb = load(cb);
+    store(ca, va);
+    if (g + 1 >= ng) break;
+    ca = piece(g + 2);
+    va = load(ca);
+    store(cb, vb);
+  }
+  // the pieces outside the pipeline
+  for (uint32_t g = 0; g < ng; g++) {
+    const uint32_t e = g * EPP + lane / J;
+    if (e >= n) continue;
+    uint32_t hp, kl, vl, ko, vo;
+    fields(e, hp, kl, vl, ko, vo);
+    const uint32_t kp = pieces16(kl), np = kp + pieces16(vl);
+    const bool first_in = j < np && (j < kp ? kl >= 16 : vl >= 8);
+    for (uint32_t q = first_in ? j + J : j; q < np; q += J) {
+      const bool key = q < kp;
+      uint8_t* dst = key ? kbase : vbase;
+      if (!dst) continue;
+      copy_piece16(dst + (key ? ko : vo), blk + (key ? hp + 10 : hp + 10 + kl), key ? kl : vl,
+                   key ? q : q - kp);
+    }
+  }
+}
+
 // One block's share of the copy (wave `sub` of `split`): per-block outputs and result totals,
 // the capacity check, then the entries -- from the walk's records `meta` (`pre` = record `lane`),
 // the block's bytes read through `src` (prefix-compressed blocks always from global memory).
@@ -1754,6 +1856,11 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
     copy_entries<16, 2, false, Src, COH>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
   } else if (LSMGPU_KNOB(p.wj, 0u) == 16 || (LSMGPU_KNOB(p.wj, 0u) == 0 && avg > 128)) {
     copy_entries<16, 2, true, Src, COH>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
+  } else if (!COH && LSMGPU_KNOB(p.wpipe, 1u) && mat && !view && n < kWave && split == 1 &&
+             !LSMGPU_KNOB(p.weo, 0u) && !ABLATE(p, 8) && !ABLATE(p, 16)) {
+    // (same box, C2 copy 0.485-0.487 -> 0.447-0.450 ms, decode 1,482 -> 1,558-1,564 GiB/s,
+    // profiles/r06p; diag build: LSMGPU_WSC_PIPE=0 keeps copy_entries below)
+    copy_entries_pipe<8>(p, blk, kbase, vbase, n, K, V, en, ek, ev, off, lane, pre);
   } else {
     // (timing-only ablations: 8 no per-entry outputs, 16 no pieces)
     if (!ABLATE(p, 8) && !LSMGPU_KNOB(p.weo, 0u)) entry_outputs<COH>(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);

@@ -264,9 +264,6 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeParams p) {
 //    loops.
 // Pieces past a lane's first (entries of more than J pieces) and streams under 16 B keep the
 // plain load -> store order.  Same bytes as encode_kernel.
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-constexpr uint32_t kNoStore = 0xfffffff0u;    // a buffer offset past any image: the store is dropped
-constexpr int kRsrcWord3 = 0x00020000;        // gfx9 buffer resource word 3 (32-bit data format)
 struct EncPass {
   uint64_t sk, sv;              // where the key / vs bytes are read
   uint32_t klen, vlen, pos, kp, np, r;
@@ -351,9 +348,7 @@ __global__ void __launch_bounds__(256) encode_pipe_kernel(EncodeParams p) {
   // hardware's range check drops it): with no branch around them the compiler counts them, so the
   // wait for the next pass's first pieces leaves them in flight (a store in a branch counts as
   // possibly absent, and the wait then drains it).  Offsets are 32-bit: an image is < 4 GiB.
-  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void*>(uniform64(reinterpret_cast<uint64_t>(out))), 0,
-      (int)(uint32_t)(dl < kNoStore ? dl : kNoStore), kRsrcWord3);
+  const __amdgpu_buffer_rsrc_t orsrc = buffer_rsrc(out, dl);
   auto put16 = [&](const u32x4& v, uint32_t o) {
     __builtin_amdgcn_raw_buffer_store_b128(v, orsrc, o, 0, 0);
   };

@@ -89,6 +89,7 @@ struct DecodeParams {
   uint32_t wcopyfuse;
   uint32_t wncop;
   uint32_t wdense;          // (diag) copy: dense piece mapping for blocks of > 128-B entries (1)
+  uint32_t wpipe;           // (diag) copy: pipelined pieces for blocks of < 64 small entries (1)
 
 };
 
