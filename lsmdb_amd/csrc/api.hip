@@ -356,7 +356,7 @@ static void decode_diag_knobs(DecodeParams& p, uint64_t nblk, uint64_t cus, uint
   p.wdpp = env("LSMGPU_WSC_DPP") && atoi(env("LSMGPU_WSC_DPP")) == 1 ? 1u : 0u;
   if (const char* v = env("LSMGPU_WSC_VIEWSCAN")) p.wview = atoi(v) == 0 ? 0u : 1u;
   if (const char* v = env("LSMGPU_WSC_DENSE")) p.wdense = atoi(v) == 0 ? 0u : 1u;
-  if (const char* v = env("LSMGPU_WSC_PIPE")) p.wpipe = atoi(v) == 0 ? 0u : 1u;
+  if (const char* v = env("LSMGPU_WSC_PIPE")) p.wpipe = (uint32_t)std::min(std::max(atoi(v), 0), 2);  // 2: any n
   const char* sl = env("LSMGPU_WSC_SLOT");
   p.wslot = sl && sl[0] == 's' ? 1u : (sl && sl[0] == 'n' ? 2u : 0u);
   (void)nblk;

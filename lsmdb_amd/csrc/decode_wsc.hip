@@ -1666,48 +1666,68 @@ __device__ __forceinline__ void copy_entries_dense(const DecodeParams& p, const 
   }
 }
 
-// The entries of a block of < 64 entries with no prefix-compressed entry, PIPELINED (materialize
-// without view; the encoder's scheme, encode.hip encode_pipe_kernel): J lanes per entry, entry
-// groups g = 0, 1, ... of 64 / J entries, records from `pre` by lane shuffle.  Each lane's first
-// piece of group g + 1 is loaded before group g's stores, and every load and store of the
-// pipeline is a range-checked buffer access all lanes issue (a lane with nothing to move gives
-// an offset past the resource: zeros read, store dropped), so the compiler's wait for group
-// g + 1's pieces counts group g's stores and leaves them in flight -- the plain copy waits
+// The entries of a block with no prefix-compressed entry, PIPELINED (materialize without view;
+// the encoder's scheme, encode.hip encode_pipe_kernel): J lanes per entry, entry groups
+// g = sub, sub + split, ... of 64 / J entries (wave `sub` of `split`).  Each lane's first piece
+// of the wave's next group is loaded before this group's stores, and every load and store of the
+// pipeline is a range-checked buffer access all lanes issue (a lane with nothing to move gives an
+// offset past the resource: zeros read, store dropped), so the compiler's wait for the next
+// group's pieces counts this group's stores and leaves them in flight -- the plain copy waits
 // (vmcnt counts stores too) for every earlier store before each piece.  In the pipeline: 16-B
 // pieces of either stream and 8-B value pieces (a 15-B value pointer's); the other pieces (key
 // streams under 16 B, value streams under 8 B, pieces past a lane's first) follow it in the
-// plain order.  key_end / val_end: one lane per entry, two buffer stores, after group 0's loads.
-template <uint32_t J>
-__device__ __forceinline__ void copy_entries_pipe(const DecodeParams& p, const uint8_t* blk,
-                                                  uint8_t* kbase, uint8_t* vbase, uint32_t n,
-                                                  uint32_t K, uint32_t V, uint64_t en, uint64_t ek,
-                                                  uint64_t ev, uint32_t off, uint32_t lane,
+// plain order.  Records come by lane shuffle from a window of 64 (`pre` for entries 0-63, then
+// loaded and waited for once per 64 entries, so no other wait sits in the pipeline);
+// key_end / val_end: one lane per entry, two buffer stores per window (by wave window % split).
+template <uint32_t J, bool COH>
+__device__ __forceinline__ void copy_entries_pipe(const DecodeParams& p, const uint32_t* meta,
+                                                  const uint8_t* blk, uint8_t* kbase, uint8_t* vbase,
+                                                  uint32_t n, uint32_t K, uint32_t V, uint64_t en,
+                                                  uint64_t ek, uint64_t ev, uint32_t off,
+                                                  uint32_t sub, uint32_t split, uint32_t lane,
                                                   uint32_t pre) {
   constexpr uint32_t EPP = kWave / J;
   const uint32_t j = lane & (J - 1);
   const __amdgpu_buffer_rsrc_t in = buffer_rsrc(blk, p.data_len - off);
   const __amdgpu_buffer_rsrc_t kr = buffer_rsrc(kbase, kbase ? K : 0u);
   const __amdgpu_buffer_rsrc_t vr = buffer_rsrc(vbase, vbase ? V : 0u);
-  // group g's pipelined piece of this lane: input offset (kNoStore: none) and destinations
-  struct Pc {
-    uint32_t src, k16, v16, v8;
-  };
+  const __amdgpu_buffer_rsrc_t ker = buffer_rsrc(p.key_end ? p.key_end + en : nullptr, p.key_end ? 4ull * n : 0ull);
+  const __amdgpu_buffer_rsrc_t ver = buffer_rsrc(p.val_end ? p.val_end + en : nullptr, p.val_end ? 4ull * n : 0ull);
+  // the record window: lane l holds record w0 + l, wx record w0 + 64
+  uint32_t w0 = 0, wr = pre, wx = n >= kWave ? ldm<COH>(meta + kWave) : 0u;
   auto fields = [&](uint32_t e, uint32_t& hp, uint32_t& kl, uint32_t& vl, uint32_t& ko, uint32_t& vo) {
-    const uint32_t ec = min(e, n - 1);
-    const uint32_t m0 = (uint32_t)__shfl((int)pre, (int)ec), m1 = (uint32_t)__shfl((int)pre, (int)ec + 1);
+    const uint32_t ec = min(e, n - 1), i = (ec - w0) & (kWave - 1);  // (off lanes: garbage, unused)
+    const uint32_t m0 = (uint32_t)__shfl((int)wr, (int)i);
+    const uint32_t nx = (uint32_t)__shfl((int)wr, (int)((i + 1) & (kWave - 1)));
+    const uint32_t m1 = i + 1 < kWave ? nx : wx;
     hp = m0 & 0xffffu;
     vo = m0 >> 16;
     vl = (m1 >> 16) - vo;
     kl = (m1 & 0xffffu) - hp - 10 - vl;  // stored key bytes
     ko = hp - 10 * ec - vo;              // (no prefix-compressed entry here)
   };
-  auto piece = [&](uint32_t g) -> Pc {
+  // key_end / val_end of the window's entries (lane = entry), written by one wave of the block's
+  // (the others issue the same stores with every offset past the end: no branch, see below)
+  auto outputs = [&]() {
+    const uint32_t e = w0 + lane;
+    uint32_t hp, kl, vl, ko, vo;
+    fields(e, hp, kl, vl, ko, vo);
+    const uint32_t o = e < n && (w0 / kWave) % split == sub ? 4 * e : kNoStore;
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(ek + ko + kl), ker, o, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(ev + vo + vl), ver, o, 0, 0);
+  };
+  // group g's pipelined piece of this lane (g past the window or the block: none): input offset
+  // (kNoStore: none) and destinations
+  struct Pc {
+    uint32_t src, k16, v16, v8;
+  };
+  auto piece = [&](uint32_t g, uint32_t g_end) -> Pc {
     const uint32_t e = g * EPP + lane / J;
     uint32_t hp, kl, vl, ko, vo;
     fields(e, hp, kl, vl, ko, vo);
     const uint32_t kp = pieces16(kl), np = kp + pieces16(vl);
     Pc c{kNoStore, kNoStore, kNoStore, kNoStore};
-    if (e < n && j < np) {
+    if (g < g_end && e < n && j < np) {
       if (j < kp) {
         if (kl >= 16) {
           const uint32_t o = min(16 * j, kl - 16);
@@ -1730,32 +1750,42 @@ __device__ __forceinline__ void copy_entries_pipe(const DecodeParams& p, const u
     __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, vr, c.v8, 0, 0);
   };
   const uint32_t ng = (n + EPP - 1) / EPP;
-  Pc ca = piece(0);
-  u32x4 va = load(ca);
-  {  // key_end / val_end of every entry (lane = entry)
-    uint32_t hp, kl, vl, ko, vo;
-    fields(lane, hp, kl, vl, ko, vo);
-    const bool on = lane < n;
-    const __amdgpu_buffer_rsrc_t ke = buffer_rsrc(p.key_end ? p.key_end + en : nullptr, p.key_end ? 4ull * n : 0ull);
-    const __amdgpu_buffer_rsrc_t ve = buffer_rsrc(p.val_end ? p.val_end + en : nullptr, p.val_end ? 4ull * n : 0ull);
-    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(ek + ko + kl), ke, on ? 4 * lane : kNoStore, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(ev + vo + vl), ve, on ? 4 * lane : kNoStore, 0, 0);
-  }
-  for (uint32_t g = 0; g < ng; g += 2) {  // two groups per trip: no register copy at the back edge
-    const Pc cb = piece(g + 1);  // (past the last group: every lane off, nothing read)
-    const u32x4 vb = load(cb);
-    store(ca, va);
-    if (g + 1 >= ng) break;
-    ca = piece(g + 2);
-    va = load(ca);
-    store(cb, vb);
+  for (uint32_t b0 = 0; b0 < n; b0 += kWave) {  // (uniform) the record windows
+    if (b0) {
+      w0 = b0;
+      wr = ldm<COH>(meta + min(b0 + lane, n));
+      wx = ldm<COH>(meta + min(b0 + kWave, n));
+    }
+    // the wave's groups of this window: g0, g0 + split, ... < g1
+    const uint32_t gw = b0 / EPP, g1 = min(ng, (b0 + kWave) / EPP);
+    const uint32_t g0 = gw + (sub + split - gw % split) % split;
+    Pc ca = piece(g0, g1);
+    u32x4 va = load(ca);
+    outputs();
+    // (a store with nothing to write: the loop is then entered with as many buffer accesses
+    // issued after the pending pieces as it loops with, so one wait count serves both entries)
+    store(Pc{kNoStore, kNoStore, kNoStore, kNoStore}, u32x4{0u, 0u, 0u, 0u});
+    for (uint32_t g = g0; g < g1; g += 2 * split) {  // two groups per trip: no register copy
+      const Pc cb = piece(g + split, g1);
+      const u32x4 vb = load(cb);
+      store(ca, va);
+      if (g + split >= g1) break;
+      ca = piece(g + 2 * split, g1);
+      va = load(ca);
+      store(cb, vb);
+    }
   }
   // the pieces outside the pipeline
-  for (uint32_t g = 0; g < ng; g++) {
+  for (uint32_t g = sub; g < ng; g += split) {
+    if (((g * EPP) & ~(kWave - 1)) != w0) {  // (uniform)
+      w0 = (g * EPP) & ~(kWave - 1);
+      wr = ldm<COH>(meta + min(w0 + lane, n));
+      wx = ldm<COH>(meta + min(w0 + kWave, n));
+    }
     const uint32_t e = g * EPP + lane / J;
-    if (e >= n) continue;
     uint32_t hp, kl, vl, ko, vo;
     fields(e, hp, kl, vl, ko, vo);
+    if (e >= n) continue;
     const uint32_t kp = pieces16(kl), np = kp + pieces16(vl);
     const bool first_in = j < np && (j < kp ? kl >= 16 : vl >= 8);
     for (uint32_t q = first_in ? j + J : j; q < np; q += J) {
@@ -1856,11 +1886,13 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
     copy_entries<16, 2, false, Src, COH>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
   } else if (LSMGPU_KNOB(p.wj, 0u) == 16 || (LSMGPU_KNOB(p.wj, 0u) == 0 && avg > 128)) {
     copy_entries<16, 2, true, Src, COH>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
-  } else if (!COH && LSMGPU_KNOB(p.wpipe, 1u) && mat && !view && n < kWave && split == 1 &&
+  } else if (!COH && LSMGPU_KNOB(p.wpipe, 1u) && mat && !view && (n < kWave || LSMGPU_KNOB(p.wpipe, 1u) == 2) &&
              !LSMGPU_KNOB(p.weo, 0u) && !ABLATE(p, 8) && !ABLATE(p, 16)) {
     // (same box, C2 copy 0.485-0.487 -> 0.447-0.450 ms, decode 1,482 -> 1,558-1,564 GiB/s,
-    // profiles/r06p; diag build: LSMGPU_WSC_PIPE=0 keeps copy_entries below)
-    copy_entries_pipe<8>(p, blk, kbase, vbase, n, K, V, en, ek, ev, off, lane, pre);
+    // profiles/r06p; diag build: LSMGPU_WSC_PIPE=0 keeps copy_entries below, =2 takes blocks of
+    // >= 64 entries too -- C4's 100-entry blocks, two waves each, lose: copy 0.0307 -> 0.0335 ms,
+    // profiles/r06q)
+    copy_entries_pipe<8, COH>(p, meta, blk, kbase, vbase, n, K, V, en, ek, ev, off, sub, split, lane, pre);
   } else {
     // (timing-only ablations: 8 no per-entry outputs, 16 no pieces)
     if (!ABLATE(p, 8) && !LSMGPU_KNOB(p.weo, 0u)) entry_outputs<COH>(p, meta, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
