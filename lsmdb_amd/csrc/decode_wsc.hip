@@ -1798,6 +1798,108 @@ __device__ __forceinline__ void copy_entries_pipe(const DecodeParams& p, const u
   }
 }
 
+// copy_entries_dense, PIPELINED (materialize without view; the scheme of copy_entries_pipe):
+// each 64-piece window's owners and piece are found (LDS marks + max-scan) and its piece loaded
+// before the previous window's stores; every pipelined load and store is a range-checked buffer
+// access all lanes issue.  Pieces of 16 B and 8 B go through the pipeline, shorter ones (streams
+// under 8 B) are copied in the plain order where they fall.
+template <bool COH>
+__device__ __forceinline__ void copy_entries_dense_pipe(const DecodeParams& p, const uint32_t* meta,
+                                                        const uint8_t* blk, uint8_t* kbase,
+                                                        uint8_t* vbase, uint32_t n, uint32_t K,
+                                                        uint32_t V, uint64_t en, uint64_t ek,
+                                                        uint64_t ev, uint32_t off, uint32_t sub,
+                                                        uint32_t split, uint32_t lane, uint32_t pre,
+                                                        uint8_t* mk) {
+  const __amdgpu_buffer_rsrc_t in = buffer_rsrc(blk, p.data_len - off);
+  const __amdgpu_buffer_rsrc_t kr = buffer_rsrc(kbase, kbase ? K : 0u);
+  const __amdgpu_buffer_rsrc_t vr = buffer_rsrc(vbase, vbase ? V : 0u);
+  const __amdgpu_buffer_rsrc_t ker = buffer_rsrc(p.key_end ? p.key_end + en : nullptr, p.key_end ? 4ull * n : 0ull);
+  const __amdgpu_buffer_rsrc_t ver = buffer_rsrc(p.val_end ? p.val_end + en : nullptr, p.val_end ? 4ull * n : 0ull);
+  struct Pc {
+    uint32_t src, dst;  // dst: stream offset; which stream and width in `kind`
+    uint32_t kind;      // 0 none, 1 key 16 B, 2 value 16 B, 3 key 8 B, 4 value 8 B
+  };
+  auto load = [&](const Pc& c) -> u32x4 {
+    return __builtin_amdgcn_raw_buffer_load_b128(in, c.kind ? c.src : kNoStore, 0, 0);
+  };
+  auto store = [&](const Pc& c, const u32x4& v) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, kr, c.kind == 1 ? c.dst : kNoStore, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(v, vr, c.kind == 2 ? c.dst : kNoStore, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, kr, c.kind == 3 ? c.dst : kNoStore, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, vr, c.kind == 4 ? c.dst : kNoStore, 0, 0);
+  };
+  for (uint32_t c0 = sub * kWave; c0 < n; c0 += split * kWave) {
+    const uint32_t e = c0 + lane;
+    const uint32_t m0 = c0 == 0 ? pre : ldm<COH>(meta + min(e, n));
+    const uint32_t nx = (uint32_t)__shfl((int)m0, (int)min(lane + 1, kWave - 1));
+    const uint32_t m1 = lane + 1 < kWave ? nx : ldm<COH>(meta + min(e + 1, n));
+    const bool on = e < n;
+    const uint32_t hp = m0 & 0xffffu, vo = m0 >> 16, hp1 = m1 & 0xffffu, vo1 = m1 >> 16;
+    const uint32_t vl = vo1 - vo, kl = hp1 - hp - 10 - vl;  // stored key bytes
+    const uint32_t ko = hp - 10 * e - vo;                   // (no prefix-compressed entry here)
+    const uint32_t kp = on && kbase ? pieces16(kl) : 0u;
+    const uint32_t pc = on ? kp + (vbase ? pieces16(vl) : 0u) : 0u;
+    const uint32_t ps = wave_scan_sat(pc, lane), ex = ps - pc;
+    const uint32_t T = __builtin_amdgcn_readlane(ps, 63);
+    uint32_t carry = 0;
+    // window r0's piece of this lane (its owner by LDS marks + max-scan, as copy_entries_dense)
+    auto win = [&](uint32_t r0) -> Pc {
+      mk[lane] = 0;
+      wave_lds_fence();
+      if (pc > 0 && ex >= r0 && ex < r0 + kWave) mk[ex - r0] = (uint8_t)(lane + 1);
+      wave_lds_fence();
+      const uint32_t own = max(wave_scan_max(mk[lane], lane), carry);  // 1 + the owner lane
+      carry = __builtin_amdgcn_readlane(own, 63);
+      wave_lds_fence();
+      const uint32_t L = own - 1;
+      const uint32_t a = (uint32_t)__shfl((int)(hp | (kl << 16)), (int)L);
+      const uint32_t c = (uint32_t)__shfl((int)(ko | (vo << 16)), (int)L);
+      const uint32_t d = (uint32_t)__shfl((int)(vl | (kp << 16)), (int)L);
+      const uint32_t exL = (uint32_t)__shfl((int)ex, (int)L);
+      const uint32_t hL = a & 0xffffu, kL = a >> 16, koL = c & 0xffffu, voL = c >> 16;
+      const uint32_t vL = d & 0xffffu, kpL = d >> 16;
+      const uint32_t P = r0 + lane;
+      Pc r{0u, 0u, 0u};
+      if (P < T) {
+        const uint32_t q = P - exL;
+        const bool key = q < kpL;
+        const uint32_t len = key ? kL : vL, qq = key ? q : q - kpL;
+        const uint32_t s0 = key ? hL + 10 : hL + 10 + kL, d0 = key ? koL : voL;
+        if (len >= 16) {
+          const uint32_t o = min(16 * qq, len - 16);
+          r = Pc{s0 + o, d0 + o, key ? 1u : 2u};
+        } else if (len >= 8) {
+          const uint32_t o = qq ? len - 8 : 0u;
+          r = Pc{s0 + o, d0 + o, key ? 3u : 4u};
+        } else {
+          copy_piece16((key ? kbase : vbase) + d0, blk + s0, len, qq);
+        }
+      }
+      return r;
+    };
+    Pc ca = win(0);
+    u32x4 va = load(ca);
+    {  // key_end / val_end (lane = entry), then a store with nothing to write: the loop is entered
+       // with as many buffer accesses after the pending piece as it loops with
+      const uint32_t o = on ? 4 * e : kNoStore;
+      __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(ek + ko + kl), ker, o, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(ev + vo1), ver, o, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, vr, kNoStore, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, vr, kNoStore, 0, 0);
+    }
+    for (uint32_t r0 = 0; r0 < T; r0 += 2 * kWave) {  // two windows per trip: no register copy
+      const Pc cb = win(r0 + kWave);
+      const u32x4 vb = load(cb);
+      store(ca, va);
+      if (r0 + kWave >= T) break;
+      ca = win(r0 + 2 * kWave);
+      va = load(ca);
+      store(cb, vb);
+    }
+  }
+}
+
 // One block's share of the copy (wave `sub` of `split`): per-block outputs and result totals,
 // the capacity check, then the entries -- from the walk's records `meta` (`pre` = record `lane`),
 // the block's bytes read through `src` (prefix-compressed blocks always from global memory).
@@ -1858,8 +1960,14 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
   // 16-lane groups fill their lanes (C3's 1.1 KB entries: dense 0.525 vs 0.496 ms; profiles/r06h)
   if (mk && avg > 128 && avg <= 512 && !LSMGPU_KNOB(p.wj, 0u) && !LSMGPU_KNOB(p.weo, 0u) &&
       LSMGPU_KNOB(p.wdense, 1u)) {
-    copy_entries_dense<COH>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view,
-                            lane, pre, mk);
+    // (pipelined: same box, C5 copy 0.550-0.555 -> 0.474-0.475 ms, decode 1,377 -> 1,533-1,538
+    // GiB/s, profiles/r06r; diag build: LSMGPU_WSC_DPIPE=0 keeps copy_entries_dense)
+    if (!COH && LSMGPU_KNOB(p.wdpipe, 1u) && mat && !view)
+      copy_entries_dense_pipe<COH>(p, meta, blk, kbase, vbase, n, K, V, en, ek, ev, off, sub, split,
+                                   lane, pre, mk);
+    else
+      copy_entries_dense<COH>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view,
+                              lane, pre, mk);
     return;
   }
   // (round 4: each lane's first piece of every entry of a pass loaded before any store left

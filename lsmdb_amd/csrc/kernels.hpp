@@ -90,6 +90,7 @@ struct DecodeParams {
   uint32_t wncop;
   uint32_t wdense;          // (diag) copy: dense piece mapping for blocks of > 128-B entries (1)
   uint32_t wpipe;           // (diag) copy: pipelined pieces for blocks of < 64 small entries (1)
+  uint32_t wdpipe;          // (diag) copy: the dense piece mapping pipelined (1)
 
 };
 
