@@ -1956,13 +1956,16 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
   // (C2: copy 0.504 -> 0.485 ms; C5 / C3 blocks of fewer, larger entries lose 3 % that way, so
   // their 16-lane groups keep writing them)
   const uint32_t avg = (K + V) / n;
-  // dense pieces for entries of 129-512 B on average (C5 copy 0.593 -> 0.547 ms); above that the
-  // 16-lane groups fill their lanes (C3's 1.1 KB entries: dense 0.525 vs 0.496 ms; profiles/r06h)
-  if (mk && avg > 128 && avg <= 512 && !LSMGPU_KNOB(p.wj, 0u) && !LSMGPU_KNOB(p.weo, 0u) &&
-      LSMGPU_KNOB(p.wdense, 1u)) {
-    // (pipelined: same box, C5 copy 0.550-0.555 -> 0.474-0.475 ms, decode 1,377 -> 1,533-1,538
-    // GiB/s, profiles/r06r; diag build: LSMGPU_WSC_DPIPE=0 keeps copy_entries_dense)
-    if (!COH && LSMGPU_KNOB(p.wdpipe, 1u) && mat && !view)
+  // dense pieces for entries of > 128 B on average.  Pipelined (materialize without view): every
+  // such block (C5 copy 0.550 -> 0.475 ms, profiles/r06r; C3's 1.1 KB entries 0.509 -> 0.469-0.474,
+  // profiles/r06s); in the plain order only up to 512 B (C5 copy 0.593 -> 0.547 ms; C3 lost,
+  // 0.525 vs 0.496 ms, profiles/r06h), above which the 16-lane groups fill their lanes
+  const bool dpipe = !COH && LSMGPU_KNOB(p.wdpipe, 1u) && mat && !view;
+  if (mk && avg > 128 && (dpipe ? avg <= LSMGPU_KNOB(p.wdmax, 0xffffffffu) : avg <= 512) &&
+      !LSMGPU_KNOB(p.wj, 0u) && !LSMGPU_KNOB(p.weo, 0u) && LSMGPU_KNOB(p.wdense, 1u)) {
+    // (diag build: LSMGPU_WSC_DPIPE=0 keeps copy_entries_dense, LSMGPU_WSC_DMAX caps the pipelined
+    // mapping's average entry)
+    if (dpipe)
       copy_entries_dense_pipe<COH>(p, meta, blk, kbase, vbase, n, K, V, en, ek, ev, off, sub, split,
                                    lane, pre, mk);
     else

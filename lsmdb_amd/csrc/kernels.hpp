@@ -91,6 +91,7 @@ struct DecodeParams {
   uint32_t wdense;          // (diag) copy: dense piece mapping for blocks of > 128-B entries (1)
   uint32_t wpipe;           // (diag) copy: pipelined pieces for blocks of < 64 small entries (1)
   uint32_t wdpipe;          // (diag) copy: the dense piece mapping pipelined (1)
+  uint32_t wdmax;           // (diag) copy: largest average entry for the pipelined dense mapping (any)
 
 };
 
