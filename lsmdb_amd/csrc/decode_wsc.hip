@@ -1666,6 +1666,30 @@ __device__ __forceinline__ void copy_entries_dense(const DecodeParams& p, const 
   }
 }
 
+// copy_entries_pipe with D - 1 entry groups' pieces in flight ahead of the stores (diag
+// LSMGPU_WSC_PDEPTH = D >= 3; one wave, one record window: at most 8 groups), the groups fully
+// unrolled so the ring of D piece registers needs no copies.
+template <int D, int NG, typename Pc, typename PF, typename LF, typename SF, typename OF>
+__device__ __forceinline__ void pipe_deep(uint32_t ng, PF&& piece, LF&& load, SF&& store, OF&& outputs) {
+  Pc c[D];
+  u32x4 v[D];
+#pragma unroll
+  for (int g = 0; g < D - 1; g++) {
+    c[g] = piece((uint32_t)g, ng);
+    v[g] = load(c[g]);
+  }
+  outputs();
+#pragma unroll
+  for (int g = 0; g < NG; g++) {
+    if ((uint32_t)g >= ng) break;  // (uniform)
+    if (g + D - 1 < NG) {
+      c[(g + D - 1) % D] = piece((uint32_t)(g + D - 1), ng);
+      v[(g + D - 1) % D] = load(c[(g + D - 1) % D]);
+    }
+    store(c[g % D], v[g % D]);
+  }
+}
+
 // The entries of a block with no prefix-compressed entry, PIPELINED (materialize without view;
 // the encoder's scheme, encode.hip encode_pipe_kernel): J lanes per entry, entry groups
 // g = sub, sub + split, ... of 64 / J entries (wave `sub` of `split`).  Each lane's first piece
@@ -1750,6 +1774,13 @@ __device__ __forceinline__ void copy_entries_pipe(const DecodeParams& p, const u
     __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, vr, c.v8, 0, 0);
   };
   const uint32_t ng = (n + EPP - 1) / EPP;
+  // blocks of one record window: two groups' pieces in flight ahead of the stores (same box,
+  // C2 copy 0.447-0.450 -> 0.440-0.441 ms; three groups ahead: 0.448, profiles/r06u)
+  const uint32_t depth = LSMGPU_KNOB(p.wpdepth, 3u);
+  if (depth >= 3 && n < kWave && split == 1) {
+    if (depth == 3) pipe_deep<3, kWave / EPP, Pc>(ng, piece, load, store, outputs);
+    else pipe_deep<4, kWave / EPP, Pc>(ng, piece, load, store, outputs);
+  } else
   for (uint32_t b0 = 0; b0 < n; b0 += kWave) {  // (uniform) the record windows
     if (b0) {
       w0 = b0;

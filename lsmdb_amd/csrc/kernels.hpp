@@ -92,6 +92,7 @@ struct DecodeParams {
   uint32_t wpipe;           // (diag) copy: pipelined pieces for blocks of < 64 small entries (1)
   uint32_t wdpipe;          // (diag) copy: the dense piece mapping pipelined (1)
   uint32_t wdmax;           // (diag) copy: largest average entry for the pipelined dense mapping (any)
+  uint32_t wpdepth;         // (diag) copy_entries_pipe: entry groups in flight + 1 (3)
 
 };
 
