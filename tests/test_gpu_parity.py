@@ -202,6 +202,51 @@ def test_device_resident_async(codec, oracle):
             assert np.array_equal(bufs.view[:n].cpu().numpy().view(np.uint64), o.view)
 
 
+@pytest.mark.parametrize("missing", ["key_data", "val_data", "ends", "keys"])
+@pytest.mark.parametrize("shape", ["c2", "c3", "c5", "short"])
+def test_partial_outputs(codec, oracle, monkeypatch, shape, missing):
+    """Materialize with some output arrays NULL (the decoded struct allows each to be absent):
+    the walk-scan-copy copies -- the pipelined 8-lane groups (C2, short entries: pieces in and
+    out of the pipeline), the pipelined dense mapping (C3, C5) -- write every array that is
+    there bit-exact against the oracle and nothing for the ones that are not (their range-checked
+    buffer stores get a zero-byte resource)."""
+    import torch
+    monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
+    if shape == "short":
+        cols, epb, bb = _random_cols(30000, 41), 0, 4096
+    else:
+        c = _cols({"c2": 2, "c3": 3, "c5": 5}[shape], {"c2": 40000, "c3": 6000, "c5": 30000}[shape], seed=43)
+        cols, epb, bb = (c.keys, c.key_end, c.vs, c.vs_end), c.entries_per_block, c.block_bytes
+    ref, _, _ = oracle.build_cols(*cols, epb, bb)
+    sst = ref + b"{}" + (2).to_bytes(4, "big")
+    off, ln, _, _ = oracle.parse_index(sst)
+    o = oracle.decode(sst, off, ln)
+    dev = torch.device("cuda", 0)
+    d_data = torch.from_numpy(np.frombuffer(sst, np.uint8).copy()).to(dev)
+    d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+    d_len = torch.from_numpy(ln.view(np.int32)).to(dev)
+    bufs = codec.alloc_decode(len(sst), int(ln.sum()), off.size, 1)
+    drop = {"key_data": ["key_data"], "val_data": ["val_data"], "ends": ["key_end", "val_end"],
+            "keys": ["key_data", "key_end"]}[missing]
+    for name in drop:
+        setattr(bufs, name, None)
+    bufs.bind()
+    codec.decode_device_async(d_data, d_off, d_len, int(ln.max()), 1, bufs)
+    codec.synchronize()
+    res = bufs.result.cpu().numpy()
+    n = o.n_entries
+    assert res[0] == n and res[5] == 0
+    assert np.array_equal(bufs.blk_first.cpu().numpy().view(np.uint32), o.blk_first)
+    if bufs.key_data is not None:
+        assert bufs.key_data[: int(res[1])].cpu().numpy().tobytes() == o.key_data.tobytes()
+    if bufs.val_data is not None:
+        assert bufs.val_data[: int(res[2])].cpu().numpy().tobytes() == o.val_data.tobytes()
+    if bufs.key_end is not None:
+        assert np.array_equal(bufs.key_end[:n].cpu().numpy().view(np.uint32), o.key_end)
+    if bufs.val_end is not None:
+        assert np.array_equal(bufs.val_end[:n].cpu().numpy().view(np.uint32), o.val_end)
+
+
 def test_capacity_overflow_reported(codec, oracle):
     c = _cols(1, 1000, seed=4)
     ref, _, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, 100, 0)
