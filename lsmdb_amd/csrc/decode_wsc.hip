@@ -1760,7 +1760,9 @@ __device__ __forceinline__ void copy_entries_pipe(const DecodeParams& p, const u
         }
       } else if (vl >= 8) {
         const uint32_t q = j - kp, o = vl >= 16 ? min(16 * q, vl - 16) : (q ? vl - 8 : 0u);
-        c.src = hp + 10 + kl + o;
+        // (an 8-B piece is read as the upper half of the 16 B ending at its last byte: the read
+        // never passes the stream's end, which may be the end of the data)
+        c.src = hp + 10 + kl + o - (vl >= 16 ? 0u : 8u);
         if (vl >= 16) c.v16 = vo + o;
         else c.v8 = vo + o;
       }
@@ -1771,7 +1773,7 @@ __device__ __forceinline__ void copy_entries_pipe(const DecodeParams& p, const u
   auto store = [&](const Pc& c, const u32x4& v) {
     __builtin_amdgcn_raw_buffer_store_b128(v, kr, c.k16, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b128(v, vr, c.v16, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, vr, c.v8, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.z, v.w}, vr, c.v8, 0, 0);
   };
   const uint32_t ng = (n + EPP - 1) / EPP;
   // blocks of one record window: two groups' pieces in flight ahead of the stores (same box,
@@ -1857,8 +1859,8 @@ __device__ __forceinline__ void copy_entries_dense_pipe(const DecodeParams& p, c
   auto store = [&](const Pc& c, const u32x4& v) {
     __builtin_amdgcn_raw_buffer_store_b128(v, kr, c.kind == 1 ? c.dst : kNoStore, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b128(v, vr, c.kind == 2 ? c.dst : kNoStore, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, kr, c.kind == 3 ? c.dst : kNoStore, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, vr, c.kind == 4 ? c.dst : kNoStore, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.z, v.w}, kr, c.kind == 3 ? c.dst : kNoStore, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.z, v.w}, vr, c.kind == 4 ? c.dst : kNoStore, 0, 0);
   };
   for (uint32_t c0 = sub * kWave; c0 < n; c0 += split * kWave) {
     const uint32_t e = c0 + lane;
@@ -1902,7 +1904,7 @@ __device__ __forceinline__ void copy_entries_dense_pipe(const DecodeParams& p, c
           r = Pc{s0 + o, d0 + o, key ? 1u : 2u};
         } else if (len >= 8) {
           const uint32_t o = qq ? len - 8 : 0u;
-          r = Pc{s0 + o, d0 + o, key ? 3u : 4u};
+          r = Pc{s0 + o - 8, d0 + o, key ? 3u : 4u};  // (the upper half of the 16 B ending here)
         } else {
           copy_piece16((key ? kbase : vbase) + d0, blk + s0, len, qq);
         }
@@ -2028,7 +2030,7 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
     copy_entries<16, 2, false, Src, COH>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
   } else if (LSMGPU_KNOB(p.wj, 0u) == 16 || (LSMGPU_KNOB(p.wj, 0u) == 0 && avg > 128)) {
     copy_entries<16, 2, true, Src, COH>(p, meta, src, kbase, vbase, n, en, ek, ev, off, sub, split, mat, view, lane, pre);
-  } else if (!COH && LSMGPU_KNOB(p.wpipe, 1u) && mat && !view && (n < kWave || LSMGPU_KNOB(p.wpipe, 1u) == 2) &&
+  } else if (!COH && p.wpipe && mat && !view && (n < kWave || p.wpipe == 2) &&
              !LSMGPU_KNOB(p.weo, 0u) && !ABLATE(p, 8) && !ABLATE(p, 16)) {
     // (same box, C2 copy 0.485-0.487 -> 0.447-0.450 ms, decode 1,482 -> 1,558-1,564 GiB/s,
     // profiles/r06p; diag build: LSMGPU_WSC_PIPE=0 keeps copy_entries below, =2 takes blocks of

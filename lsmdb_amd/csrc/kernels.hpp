@@ -89,7 +89,7 @@ struct DecodeParams {
   uint32_t wcopyfuse;
   uint32_t wncop;
   uint32_t wdense;          // (diag) copy: dense piece mapping for blocks of > 128-B entries (1)
-  uint32_t wpipe;           // (diag) copy: pipelined pieces for blocks of < 64 small entries (1)
+  uint32_t wpipe;           // copy: pipelined 8-lane groups for blocks of < 64 entries (1), of any (2)
   uint32_t wdpipe;          // (diag) copy: the dense piece mapping pipelined (1)
   uint32_t wdmax;           // (diag) copy: largest average entry for the pipelined dense mapping (any)
   uint32_t wpdepth;         // (diag) copy_entries_pipe: entry groups in flight + 1 (3)

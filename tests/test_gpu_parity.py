@@ -247,6 +247,50 @@ def test_partial_outputs(codec, oracle, monkeypatch, shape, missing):
         assert np.array_equal(bufs.val_end[:n].cpu().numpy().view(np.uint32), o.val_end)
 
 
+@pytest.mark.parametrize("last", ["small", "large"])
+def test_pieces_at_data_end(codec, oracle, monkeypatch, last):
+    """The pipelined copies read 16 B per piece through a resource ending at the data's end: the
+    batch's last block has no terminator (the iterator ends it at its length, iterator.go:115-118)
+    and ends exactly at the end of `data`, with value streams of 8-15 B last (8-B pieces) and of
+    16+ B -- small entries (the 8-lane groups) or one large key (the dense mapping)."""
+    import struct
+    import torch
+    monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
+    c = _cols(2, 40000, seed=47)
+    ref, _, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, 0, 4096)
+    off, ln, _, _ = oracle.parse_index(ref + b"{}" + (2).to_bytes(4, "big"))
+    data = bytearray(ref[: int(off[-1]) + int(ln[-1])])
+    rng = np.random.default_rng(5)
+    blk, prev = b"", 0xFFFFFFFF
+    shapes = [(16, 12), (16, 100), (16, 9), (16, 15), (16, 8)] if last == "small" else [(200, 12), (180, 9)]
+    for kl, vl in shapes:
+        key, val = rng.bytes(kl), rng.bytes(vl)
+        pos = len(blk)
+        blk += struct.pack(">HHHI", 0, kl, vl, prev) + key + val
+        prev = pos
+    b0 = len(data)
+    data += blk
+    offs = np.append(off, b0).astype(np.uint32)
+    lens = np.append(ln, len(blk)).astype(np.uint32)
+    sst = bytes(data)
+    o = oracle.decode(sst, offs, lens)
+    assert o.blk_status[-1] == 0 and o.n_entries > len(shapes)
+    dev = torch.device("cuda", 0)
+    d_data = torch.from_numpy(np.frombuffer(sst, np.uint8).copy()).to(dev)
+    d_off = torch.from_numpy(offs.view(np.int32)).to(dev)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+    bufs = codec.alloc_decode(len(sst), int(lens.sum()), offs.size, 1)
+    codec.decode_device_async(d_data, d_off, d_len, int(lens.max()), 1, bufs, data_len=len(sst))
+    codec.synchronize()
+    res = bufs.result.cpu().numpy()
+    n = o.n_entries
+    assert res[0] == n and res[5] == 0
+    assert bufs.key_data[: int(res[1])].cpu().numpy().tobytes() == o.key_data.tobytes()
+    assert bufs.val_data[: int(res[2])].cpu().numpy().tobytes() == o.val_data.tobytes()
+    assert np.array_equal(bufs.key_end[:n].cpu().numpy().view(np.uint32), o.key_end)
+    assert np.array_equal(bufs.val_end[:n].cpu().numpy().view(np.uint32), o.val_end)
+
+
 def test_capacity_overflow_reported(codec, oracle):
     c = _cols(1, 1000, seed=4)
     ref, _, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, 100, 0)
