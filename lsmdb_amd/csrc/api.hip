@@ -337,7 +337,10 @@ static void decode_diag_knobs(DecodeParams& p, uint64_t nblk, uint64_t cus, uint
   if (p.wj != 8 && p.wj != 16) p.wj = 0;
   if (const char* v = env("LSMGPU_WSC_CHUNK")) p.wchunk = atoi(v) == 16 ? 16u : 32u;
   if (const char* v = env("LSMGPU_WSC_VIEWKEEP")) p.wkeep = atoi(v) == 0 ? 0u : 1u;
-  if (const char* v = env("LSMGPU_WSC_TILE")) p.wtile = atoi(v) == 192 ? 192u : 256u;
+  if (const char* v = env("LSMGPU_WSC_TILE")) {
+    const int t = atoi(v);
+    p.wtile = t == 192 || t == 128 || t == 64 ? (uint32_t)t : 256u;
+  }
   p.walign = env("LSMGPU_WSC_ALIGN") ? (uint32_t)atoi(env("LSMGPU_WSC_ALIGN")) : 0u;
   if (const char* v = env("LSMGPU_WSC_LOOKBACK")) p.wlbfull = strcmp(v, "window") == 0 ? 0u : 1u;
   if (const char* v = env("LSMGPU_WSC_BIDIR")) p.wbidir = (uint32_t)std::min(std::max(atoi(v), 0), 2);
@@ -359,6 +362,8 @@ static void decode_diag_knobs(DecodeParams& p, uint64_t nblk, uint64_t cus, uint
   if (const char* v = env("LSMGPU_WSC_PIPE")) p.wpipe = (uint32_t)std::min(std::max(atoi(v), 0), 2);  // 2: any n
   if (const char* v = env("LSMGPU_WSC_DPIPE")) p.wdpipe = atoi(v) == 0 ? 0u : 1u;
   if (const char* v = env("LSMGPU_WSC_DMAX")) p.wdmax = (uint32_t)atoi(v);
+  if (const char* v = env("LSMGPU_WSC_DMIN")) p.wdmin = (uint32_t)atoi(v);
+  if (const char* v = env("LSMGPU_WSC_LBIDIR")) p.wlbidir = atoi(v) == 0 ? 0u : 1u;
   if (const char* v = env("LSMGPU_WSC_PDEPTH")) p.wpdepth = (uint32_t)std::min(std::max(atoi(v), 2), 4);
   const char* sl = env("LSMGPU_WSC_SLOT");
   p.wslot = sl && sl[0] == 's' ? 1u : (sl && sl[0] == 'n' ? 2u : 0u);
@@ -463,6 +468,9 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     // the diagnostic build's defaults of its extra knobs are the product's fixed choices
     p.wchunk = 32u;
     p.wkeep = 1u;
+    // lane walks without wide tiles: 256-block tiles (128 / 64 when 256-block tiles would leave CUs
+    // without one measured equal -- C5 walk 0.1831-0.1837 vs 0.1805-0.1824 ms, profiles/r06z --
+    // so they stay in the diagnostic build, LSMGPU_WSC_TILE)
     p.wtile = 256u;
     p.wlbfull = 1u;
     p.wbidir = 1u;
@@ -476,7 +484,9 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     p.wpipe = nblk > 64ull * cus ? 2u : 1u;
     p.wdpipe = 1u;
     p.wdmax = 0xffffffffu;
+    p.wdmin = 128u;
     p.wpdepth = 3u;
+    p.wlbidir = 0u;
 #ifdef LSMGPU_DIAG
     decode_diag_knobs(p, nblk, cus, max_blk_len, wk_env);
     // group walks: the copy in the walk's launch (LSMGPU_WSC_COPYFUSE=1), by workgroups past the

@@ -1994,7 +1994,7 @@ __device__ __forceinline__ void copy_block(const DecodeParams& p, uint32_t b, co
   // profiles/r06s); in the plain order only up to 512 B (C5 copy 0.593 -> 0.547 ms; C3 lost,
   // 0.525 vs 0.496 ms, profiles/r06h), above which the 16-lane groups fill their lanes
   const bool dpipe = !COH && LSMGPU_KNOB(p.wdpipe, 1u) && mat && !view;
-  if (mk && avg > 128 && (dpipe ? avg <= LSMGPU_KNOB(p.wdmax, 0xffffffffu) : avg <= 512) &&
+  if (mk && avg > LSMGPU_KNOB(p.wdmin, 128u) && (dpipe ? avg <= LSMGPU_KNOB(p.wdmax, 0xffffffffu) : avg <= 512) &&
       !LSMGPU_KNOB(p.wj, 0u) && !LSMGPU_KNOB(p.weo, 0u) && LSMGPU_KNOB(p.wdense, 1u)) {
     // (diag build: LSMGPU_WSC_DPIPE=0 keeps copy_entries_dense, LSMGPU_WSC_DMAX caps the pipelined
     // mapping's average entry)
@@ -2303,6 +2303,278 @@ __global__ void __launch_bounds__(TB) wsc_walk_persist_kernel(DecodeParams p) {
   }
 }
 
+// The lane walk with a second lane per block walking it BACKWARD (round 6; materialize or view
+// through the copy launch; batches of long blocks: C5's 150-entry chains).  A wave holds 32
+// blocks: lane l < 32 walks block l forward exactly as the lane walk does, lane l + 32 walks it
+// backward from the terminator T = len - 13 along the headers' `prev` fields (builder.go:95-99,
+// 121-123).  The iterator never reads `prev`, so a backward step is accepted only when the
+// entry it names is one the iterator would accept there: not a terminator, 10 + plen <= len,
+// plen == 0 if it is at 0, and ending exactly where the last accepted one starts
+// (pos + 10 + klen + vlen == bx).  Every accepted entry therefore lies on the forward chain once
+// the forward walk reaches the lowest one, bx: the forward lane stops walking when its position
+// equals its partner's bx and takes the backward entries from the partner's LDS stack instead
+// (one LDS read per entry, no HBM round trip), then ends at T as the iterator does.  Partners
+// meet through lane shuffles, once per step; both directions' header loads go out before one
+// wait.  A backward lane stops when its stack is full (kBackCap), when a candidate fails, or when
+// the forward lane has passed the candidate; if the forward walk never lands on bx (a block the
+// Builder did not write) it simply walks on to its end: the result is always the forward
+// iterator's.  Records, flushes, tile scan, look-back and epilogue are the lane walk's.
+constexpr uint32_t kBackCap = 96;  // backward entries per block (LDS stack)
+
+__device__ __forceinline__ void load_hdr2_nt(const uint8_t* g, uint32_t& w0, uint32_t& w1,
+                                             uint32_t& x1) {
+  typedef unsigned int v2 __attribute__((ext_vector_type(2)));
+  v2 a, c;
+  // header bytes [0, 8) and [2, 10): plen klen vlen, and prev (bytes 6-9 = c.y)
+  asm volatile("global_load_dwordx2 %0, %2, off nt\n\tglobal_load_dwordx2 %1, %3, off nt"
+               : "=v"(a), "=v"(c) : "v"(g), "v"(g + 2) : "memory");
+  w0 = a.x;
+  w1 = a.y;
+  x1 = c.y;
+}
+
+template <uint32_t TB>
+__global__ void __launch_bounds__(2 * TB) wsc_walk_bidir_kernel(DecodeParams p) {
+  constexpr uint32_t CH = 32, kThreads = 2 * TB, kWaves = kThreads / kWave, kStage = CH + 1;
+  constexpr uint32_t kHalf = kWave / 2;  // blocks per wave
+  static_assert(TB % kHalf == 0, "whole waves");
+  __shared__ __attribute__((aligned(16))) uint32_t stage[TB * kStage];
+  __shared__ uint32_t bstk[TB * kBackCap];
+  __shared__ uint32_t s_tile;
+  __shared__ uint32_t s_wave[kWaves][3];
+  __shared__ uint32_t s_part[kWaves][3];
+  __shared__ uint32_t s_ex[3];
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const bool fwd = lane < kHalf;
+  const uint32_t tb = wave * kHalf + (lane & (kHalf - 1)), partner = lane ^ kHalf;
+  const uint32_t ntiles = (p.nblk + TB - 1) / TB;
+  if (tid == 0) {
+    const uint32_t t = atomicAdd(p.gcnt, 1u);
+    if (t == ntiles - 1) atomicExch(p.gcnt, 0u);  // every ticket is taken
+    s_tile = t;
+  }
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  if (p.zero_result && tile == 0 && tid < 8)  // (as wsc_walk_kernel: before anything else)
+    atomicExch(reinterpret_cast<unsigned long long*>(p.result + tid), 0ull);
+  const uint32_t b = tile * TB + tb;
+  const bool valid = b < p.nblk;
+  uint32_t off = 0, len = 0, st = LSMGPU_BLK_OK;
+  if (valid) {
+    off = p.blk_off[b];
+    len = p.blk_len[b];
+  }
+  bool done = !valid;
+  if (valid && (uint64_t)off + len > p.data_len) {
+    st = LSMGPU_BLK_RANGE;
+    done = true;
+  }
+  const uint8_t* blk = p.data + off;
+  uint32_t* const row = stage + tb * kStage;
+  uint32_t* const stk = bstk + tb * kBackCap;
+  const uint32_t wb0 = tile * TB + wave * kHalf;
+  // forward: the lane walk's state; drain: taking the partner's backward entries
+  uint32_t n = 0, K = 0, V = 0, pos = 0, dn = 0, di = 0, dk = 0;
+  bool drain = false;
+  // backward: lowest accepted position bx (T before the first entry), its prev `by`, entries bn
+  // on the stack, their key / value bytes; bstart: the terminator has been read
+  uint32_t bx = len - 13, by = 0, bn = 0, bk = 0;
+  bool bact = !fwd && !done && len >= 23, bstart = false;
+  if (fwd) bx = 0;
+  for (uint32_t k = 0;; k++) {
+    if (__ballot(fwd && !done) == 0) break;  // (the backward lanes only serve the forward ones)
+    // partners: the forward lane sees the backward chain's lowest entry and its size, the
+    // backward lane the forward position (and whether that walk has ended)
+    const uint32_t s_low = (uint32_t)__shfl((int)bx, (int)partner);
+    const uint32_t s_bn = (uint32_t)__shfl((int)(bstart ? bn : 0u), (int)partner);
+    const uint32_t s_bk = (uint32_t)__shfl((int)bk, (int)partner);
+    const uint32_t s_pos = (uint32_t)__shfl((int)pos, (int)partner);
+    const uint32_t s_done = (uint32_t)__shfl((int)(done ? 1u : 0u), (int)partner);
+    bool gl = false;
+    uint32_t ga = 0;
+    if (fwd && !done) {
+      if (!drain && s_bn > 0 && pos == s_low) {  // met: the rest are the partner's entries
+        drain = true;
+        dn = s_bn;
+        dk = s_bk;
+      }
+      if (!drain) {
+        if (pos >= len) done = true;                                                // iterator.go:115-118
+        else if (len - pos < 10) { st = LSMGPU_BLK_TRUNC_HEADER; done = true; }
+        else { gl = true; ga = pos; }
+      }
+    }
+    if (!fwd && bact) {
+      if (s_done || bn == kBackCap) bact = false;
+      // (no entry fits; or the forward walk reads the candidate this step or has passed it: it
+      // lands on bx by itself if the chains agree)
+      else if (bstart && (by > bx || bx - by < 10 || by <= s_pos)) bact = false;
+      else { gl = true; ga = bstart ? by : bx; }
+    }
+    uint32_t w0 = 0, w1 = 0, x1 = 0;
+    if (gl) load_hdr2_nt(blk + ga, w0, w1, x1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (one round trip for both directions)
+    const uint32_t plen = __builtin_amdgcn_perm(0u, w0, 0x0c0c0001u);
+    const uint32_t klen = __builtin_amdgcn_perm(0u, w0, 0x0c0c0203u);
+    const uint32_t vlen = __builtin_amdgcn_perm(0u, w1, 0x0c0c0001u);
+    bool rec = false;
+    if (fwd && !done) {
+      if (drain) {
+        wave_lds_fence();
+        const uint32_t e = stk[dn - 1 - di];  // ascending positions: the stack's top is the last
+        row[n & (CH - 1)] = (e & 0xffffu) | (V << 16);
+        V += e >> 16;
+        n++;
+        di++;
+        rec = true;
+        if (di == dn) {  // at the terminator, as the iterator
+          done = true;
+          pos = len - 13;
+          K += dk;
+        }
+      } else if (gl) {
+        do {
+          if ((klen | plen) == 0) { done = true; break; }          // iterator.go:124-127
+          if (n == 0 && plen != 0) { st = LSMGPU_BLK_FIRST_PLEN; done = true; break; }
+          if (10 + plen > len) { st = LSMGPU_BLK_PREFIX_OOB; done = true; break; }
+          const uint32_t end = pos + 10 + klen + vlen;             // iterator.go:101-109
+          if (end > len) { st = LSMGPU_BLK_VALUE_OVERFLOW; done = true; break; }
+          row[n & (CH - 1)] = pos | (V << 16);
+          K += plen + klen;
+          V += vlen;
+          n++;
+          pos = end;
+          rec = true;
+        } while (false);
+      }
+    }
+    if (!fwd && gl) {
+      const uint32_t prev = __builtin_bswap32(x1);
+      if (!bstart) {  // the terminator: T's prev names the last entry
+        bstart = true;
+        if ((klen | plen) == 0 && prev != 0xffffffffu && prev + 10 <= bx) by = prev;
+        else bact = false;
+      } else if ((klen | plen) != 0 && by + 10 + klen + vlen == bx && 10 + plen <= len &&
+                 (by != 0 || plen == 0)) {
+        stk[bn] = by | (vlen << 16);
+        wave_lds_fence();
+        bn++;
+        bk += plen + klen;
+        bx = by;
+        by = prev;
+      } else {
+        bact = false;
+      }
+    }
+    if ((k & (CH - 1)) == CH - 1) {  // whole 128-B record lines of the forward rows, 8 lanes per line
+      const uint64_t fl = __ballot(rec);
+      if (fl) {
+        wave_lds_fence();
+        constexpr uint32_t kPer = CH / 4;
+#pragma unroll
+        for (uint32_t q = 0; q < kHalf / (kWave / kPer); q++) {
+          const uint32_t L = (kWave / kPer) * q + lane / kPer, part = lane % kPer;
+          if ((fl >> L) & 1ull) {
+            const uint32_t* rw = stage + (wave * kHalf + L) * kStage + 4 * part;
+            uint32_t* mL = p.wmeta + (uint64_t)(wb0 + L) * p.wcap + (k - (CH - 1));
+            reinterpret_cast<uint4*>(mL)[part] = make_uint4(rw[0], rw[1], rw[2], rw[3]);
+          }
+        }
+        wave_lds_fence();
+      }
+    }
+  }
+  const bool own = fwd && valid;  // the lane that reports the block
+  if (own) row[n & (CH - 1)] = pos | (V << 16);  // the sentinel
+  const uint64_t vm = __ballot(own);
+  wave_lds_fence();
+  {
+    constexpr uint32_t kPer = CH / 4;
+#pragma unroll
+    for (uint32_t q = 0; q < kHalf / (kWave / kPer); q++) {
+      const uint32_t L = (kWave / kPer) * q + lane / kPer, part = lane % kPer;
+      const uint32_t nL = (uint32_t)__shfl((int)n, (int)L);
+      if ((vm >> L) & 1ull) {
+        const uint32_t* rw = stage + (wave * kHalf + L) * kStage + 4 * part;
+        uint32_t* mL = p.wmeta + (uint64_t)(wb0 + L) * p.wcap + (nL & ~(CH - 1));
+        reinterpret_cast<uint4*>(mL)[part] = make_uint4(rw[0], rw[1], rw[2], rw[3]);
+      }
+    }
+  }
+  if (!fwd) n = K = V = 0;
+  if (own && K != pos - 10 * n - V) st |= kPlenFlag;  // (the descriptor's status word)
+  // tile scan (backward lanes add nothing), the tile's aggregate, look-back, epilogue
+  const uint32_t in = wave_scan_sat(n, lane), ik = wave_scan_sat(K, lane), iv = wave_scan_sat(V, lane);
+  if (lane == 63) {
+    s_wave[wave][0] = in;
+    s_wave[wave][1] = ik;
+    s_wave[wave][2] = iv;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    uint32_t tn = 0, tk = 0, tv = 0;
+    for (uint32_t w = 0; w < kWaves; w++) {
+      tn = sat_add(tn, s_wave[w][0]);
+      tk = sat_add(tk, s_wave[w][1]);
+      tv = sat_add(tv, s_wave[w][2]);
+    }
+    store3(p.lb + (uint64_t)tile * 8, p.tag, tn, tk, tv, lane);
+  }
+  Tot part{0, 0, 0};
+  if (tile > 0) part = lookback_partial(p.lb, tile, p.tag, tid, kThreads, p.result);
+  const uint32_t pn = wave_sum_sat(part.n), pk = wave_sum_sat(part.k), pv = wave_sum_sat(part.v);
+  if (lane == 0) {
+    s_part[wave][0] = pn;
+    s_part[wave][1] = pk;
+    s_part[wave][2] = pv;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    Tot ex{0, 0, 0};
+    for (uint32_t w = 0; w < kWaves; w++) {
+      ex.n = sat_add(ex.n, s_part[w][0]);
+      ex.k = sat_add(ex.k, s_part[w][1]);
+      ex.v = sat_add(ex.v, s_part[w][2]);
+    }
+    s_ex[0] = ex.n;
+    s_ex[1] = ex.k;
+    s_ex[2] = ex.v;
+  }
+  __syncthreads();
+  if (own) {
+    uint32_t on = s_ex[0], ok = s_ex[1], ov = s_ex[2];
+    for (uint32_t w = 0; w < wave; w++) {
+      on = sat_add(on, s_wave[w][0]);
+      ok = sat_add(ok, s_wave[w][1]);
+      ov = sat_add(ov, s_wave[w][2]);
+    }
+    const uint32_t sw = st, stc = sw & ~kPlenFlag;
+    const uint32_t en = sat_add(on, in - n), ek = sat_add(ok, ik == 0xffffffffu ? ik : ik - K),
+                   ev = sat_add(ov, iv - V);
+    p.wdesc[2ull * b] = make_uint4(n, K, V, sw);
+    p.wdesc[2ull * b + 1] = make_uint4(en, ek, ev, off);
+    if (p.blk_first) p.blk_first[b] = en;
+    if (p.blk_status) p.blk_status[b] = (int32_t)stc;
+    if (stc != LSMGPU_BLK_OK) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(p.result + 4), 1ull);
+      atomicMax(reinterpret_cast<unsigned long long*>(p.result + 3), (unsigned long long)(p.nblk - b));
+    }
+    if (b == p.nblk - 1) {  // totals of the whole batch
+      if (p.blk_first) p.blk_first[p.nblk] = (uint32_t)((uint64_t)en + n);
+      p.result[0] = (uint64_t)en + n;
+      p.result[1] = (uint64_t)ek + K;
+      p.result[2] = (uint64_t)ev + V;
+    }
+    bool fits = (uint64_t)en + n <= p.ent_cap && (uint64_t)en + n <= 0xffffffffull;
+    if (p.mode & LSMGPU_MODE_MATERIALIZE) {  // the copy's output streams
+      const uint64_t kend = (uint64_t)ek + K, vend = (uint64_t)ev + V;
+      fits = fits && (kend <= p.key_cap || !p.key_data) && (vend <= p.val_cap || !p.val_data) &&
+             kend < 0xffffffffull && vend <= 0xffffffffull;
+    }
+    if (!fits) atomicOr(reinterpret_cast<unsigned long long*>(p.result + 5), 1ull);
+  }
+}
+
 hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mid) {
   const uint32_t nblk = p.nblk;
   // the adopted walks (api.hip picks one per batch; the parity suite runs each of them):
@@ -2361,13 +2633,24 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 256>), dim3((nblk + 255) / 256), dim3(256), p.wpad, s, p);
   }
 #endif
+  else if (LSMGPU_KNOB(p.wlbidir, 0u) && !p.wfuse)  // a backward lane per block (batches of long blocks)
+    hipLaunchKernelGGL(wsc_walk_bidir_kernel<128>, dim3((nblk + 127) / 128), dim3(256), 0, s, p);
+#ifdef LSMGPU_DIAG
+  // fewer 256-block tiles than CUs (C5 2^30 B: 32 K blocks of 32 KiB, 128 tiles): smaller tiles
+  // so that every CU walks (measured equal, profiles/r06z)
+  else if (p.wtile == 128)
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 128>), dim3((nblk + 127) / 128), dim3(128), 0, s, p);
+  else if (p.wtile == 64)
+    hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 64>), dim3((nblk + 63) / 64), dim3(64), 0, s, p);
+#endif
   else
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 256>), dim3((nblk + 255) / 256), dim3(256), 0, s, p);
   hipError_t e = hipGetLastError();
 #ifdef LSMGPU_STAMPS
   if (e == hipSuccess && p.stamps && !persist) {  // diagnostics: the walk's per-tile timeline
     const uint32_t tb = p.wwalk == kWalkGroup ? (p.wbidir && p.wlanes == 8 ? 16 / p.wbidir : 256 / p.wlanes)
-                      : (p.wwide ? p.wtbe : (p.wfuse && p.wkeep && p.wtile == 192) || p.wtile == 192 ? 192 : 256);
+                      : (p.wwide ? p.wtbe : (p.wfuse && p.wkeep && p.wtile == 192) || p.wtile == 192 ? 192
+                         : p.wtile == 128 || p.wtile == 64 ? p.wtile : 256);
     const uint32_t nt = (nblk + tb - 1) / tb;
     std::vector<uint64_t> h((size_t)nt * 4);
     uint64_t cnt[4];

@@ -69,7 +69,7 @@ struct DecodeParams {
   uint32_t zero_result;     // walk-scan-copy with a copy launch: the walk zeroes result[0..7]
   uint32_t wchunk;          // lane walk: records per flushed chunk (16 or 32)
   uint32_t wkeep;           // view-only lane walk: records kept in LDS (kWalkLaneView)
-  uint32_t wtile;           // lane walks: blocks (= threads) per workgroup, 192 or 256
+  uint32_t wtile;           // lane walks: blocks (= threads) per workgroup: 256 ((diag) 64, 128, 192)
   uint32_t walign;          // copy: aligned 16-B output chunks for blocks of <= 63 entries
   uint32_t wwide;           // lane walks: 0 (256-block tiles, 4 per CU) or 576 (2 per CU)
   uint32_t wlbfull;         // walk: every thread of a tile sums predecessor aggregates (no windows)
@@ -92,7 +92,9 @@ struct DecodeParams {
   uint32_t wpipe;           // copy: pipelined 8-lane groups for blocks of < 64 entries (1), of any (2)
   uint32_t wdpipe;          // (diag) copy: the dense piece mapping pipelined (1)
   uint32_t wdmax;           // (diag) copy: largest average entry for the pipelined dense mapping (any)
+  uint32_t wdmin;           // (diag) copy: the dense mapping above this average entry (128)
   uint32_t wpdepth;         // (diag) copy_entries_pipe: entry groups in flight + 1 (3)
+  uint32_t wlbidir;         // lane walk: a second lane per block walking backward
 
 };
 
