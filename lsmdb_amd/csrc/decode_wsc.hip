@@ -2321,16 +2321,24 @@ __global__ void __launch_bounds__(TB) wsc_walk_persist_kernel(DecodeParams p) {
 // iterator's.  Records, flushes, tile scan, look-back and epilogue are the lane walk's.
 constexpr uint32_t kBackCap = 96;  // backward entries per block (LDS stack)
 
-__device__ __forceinline__ void load_hdr2_nt(const uint8_t* g, uint32_t& w0, uint32_t& w1,
-                                             uint32_t& x1) {
+// header bytes [0, 8): plen klen vlen (no wait: the caller waits once for every direction)
+__device__ __forceinline__ void load_hdr_nt(const uint8_t* g, uint32_t& w0, uint32_t& w1) {
   typedef unsigned int v2 __attribute__((ext_vector_type(2)));
-  v2 a, c;
-  // header bytes [0, 8) and [2, 10): plen klen vlen, and prev (bytes 6-9 = c.y)
-  asm volatile("global_load_dwordx2 %0, %2, off nt\n\tglobal_load_dwordx2 %1, %3, off nt"
-               : "=v"(a), "=v"(c) : "v"(g), "v"(g + 2) : "memory");
+  v2 a;
+  asm volatile("global_load_dwordx2 %0, %1, off nt" : "=v"(a) : "v"(g) : "memory");
   w0 = a.x;
   w1 = a.y;
-  x1 = c.y;
+}
+// the 16 B at g (a header at g + 6: plen, klen, vlen, prev in bytes 6-15)
+__device__ __forceinline__ void load_hdr16_nt(const uint8_t* g, uint32_t& w0, uint32_t& w1,
+                                              uint32_t& w2, uint32_t& w3) {
+  typedef unsigned int v4 __attribute__((ext_vector_type(4)));
+  v4 a;
+  asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(a) : "v"(g) : "memory");
+  w0 = a.x;
+  w1 = a.y;
+  w2 = a.z;
+  w3 = a.w;
 }
 
 template <uint32_t TB>
@@ -2373,80 +2381,74 @@ __global__ void __launch_bounds__(2 * TB) wsc_walk_bidir_kernel(DecodeParams p) 
   uint32_t* const row = stage + tb * kStage;
   uint32_t* const stk = bstk + tb * kBackCap;
   const uint32_t wb0 = tile * TB + wave * kHalf;
-  // forward: the lane walk's state; drain: taking the partner's backward entries
-  uint32_t n = 0, K = 0, V = 0, pos = 0, dn = 0, di = 0, dk = 0;
-  bool drain = false;
+  // forward: the lane walk's state; met: it reached the partner's lowest backward entry
+  uint32_t n = 0, K = 0, V = 0, pos = 0;
+  bool met = false;
   // backward: lowest accepted position bx (T before the first entry), its prev `by`, entries bn
-  // on the stack, their key / value bytes; bstart: the terminator has been read
+  // on the stack, their key bytes bk; bstart: the terminator has been read
   uint32_t bx = len - 13, by = 0, bn = 0, bk = 0;
   bool bact = !fwd && !done && len >= 23, bstart = false;
   if (fwd) bx = 0;
+  [[maybe_unused]] uint32_t steps = 0;
   for (uint32_t k = 0;; k++) {
-    if (__ballot(fwd && !done) == 0) break;  // (the backward lanes only serve the forward ones)
-    // partners: the forward lane sees the backward chain's lowest entry and its size, the
-    // backward lane the forward position (and whether that walk has ended)
-    const uint32_t s_low = (uint32_t)__shfl((int)bx, (int)partner);
-    const uint32_t s_bn = (uint32_t)__shfl((int)(bstart ? bn : 0u), (int)partner);
-    const uint32_t s_bk = (uint32_t)__shfl((int)bk, (int)partner);
-    const uint32_t s_pos = (uint32_t)__shfl((int)pos, (int)partner);
-    const uint32_t s_done = (uint32_t)__shfl((int)(done ? 1u : 0u), (int)partner);
+    if (__ballot(fwd && !done && !met) == 0) break;  // (the backward lanes only serve the forward ones)
+    steps = k + 1;
+    // partners, one shuffle: the forward lane sees the backward chain's lowest entry and its
+    // size, the backward lane the forward position and whether that walk has stopped (positions
+    // are < 64 KiB, stacks < 32 K entries)
+    const uint32_t mine = fwd ? pos | ((done || met) ? 1u << 16 : 0u)
+                              : bx | ((bstart ? bn : 0u) << 16);
+    const uint32_t his = (uint32_t)__shfl((int)mine, (int)partner);
     bool gl = false;
     uint32_t ga = 0;
-    if (fwd && !done) {
-      if (!drain && s_bn > 0 && pos == s_low) {  // met: the rest are the partner's entries
-        drain = true;
-        dn = s_bn;
-        dk = s_bk;
-      }
-      if (!drain) {
-        if (pos >= len) done = true;                                                // iterator.go:115-118
-        else if (len - pos < 10) { st = LSMGPU_BLK_TRUNC_HEADER; done = true; }
-        else { gl = true; ga = pos; }
+    if (fwd && !done && !met) {
+      if ((his >> 16) != 0 && pos == (his & 0xffffu)) {  // met: the rest are the partner's entries
+        met = true;
+      } else if (pos >= len) {
+        done = true;                                                               // iterator.go:115-118
+      } else if (len - pos < 10) {
+        st = LSMGPU_BLK_TRUNC_HEADER;
+        done = true;
+      } else {
+        gl = true;
+        ga = pos;
       }
     }
     if (!fwd && bact) {
-      if (s_done || bn == kBackCap) bact = false;
+      const uint32_t s_pos = his & 0xffffu;
+      if ((his >> 16) != 0 || bn == kBackCap) bact = false;
       // (no entry fits; or the forward walk reads the candidate this step or has passed it: it
       // lands on bx by itself if the chains agree)
-      else if (bstart && (by > bx || bx - by < 10 || by <= s_pos)) bact = false;
+      else if (bstart && (by > bx || bx - by < 10 || by <= s_pos || by < 6)) bact = false;
       else { gl = true; ga = bstart ? by : bx; }
     }
-    uint32_t w0 = 0, w1 = 0, x1 = 0;
-    if (gl) load_hdr2_nt(blk + ga, w0, w1, x1);
+    // one load instruction for the wave: every lane the 16 B ending with its header (bytes 6-15:
+    // plen, klen, vlen, prev; the entry is inside the block, so the read is); the header at 0
+    // (every forward lane's first step) as 8 B of its own
+    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+    const bool at0 = ga < 6;
+    if (gl && !at0) load_hdr16_nt(blk + ga - 6, w0, w1, w2, w3);
+    if (gl && at0) load_hdr_nt(blk + ga, w0, w1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (one round trip for both directions)
-    const uint32_t plen = __builtin_amdgcn_perm(0u, w0, 0x0c0c0001u);
-    const uint32_t klen = __builtin_amdgcn_perm(0u, w0, 0x0c0c0203u);
-    const uint32_t vlen = __builtin_amdgcn_perm(0u, w1, 0x0c0c0001u);
+    const uint32_t plen = at0 ? __builtin_amdgcn_perm(0u, w0, 0x0c0c0001u) : __builtin_amdgcn_perm(0u, w1, 0x0c0c0203u);
+    const uint32_t klen = at0 ? __builtin_amdgcn_perm(0u, w0, 0x0c0c0203u) : __builtin_amdgcn_perm(0u, w2, 0x0c0c0001u);
+    const uint32_t vlen = at0 ? __builtin_amdgcn_perm(0u, w1, 0x0c0c0001u) : __builtin_amdgcn_perm(0u, w2, 0x0c0c0203u);
+    const uint32_t x1 = w3;  // (backward lanes: never at 0)
     bool rec = false;
-    if (fwd && !done) {
-      if (drain) {
-        wave_lds_fence();
-        const uint32_t e = stk[dn - 1 - di];  // ascending positions: the stack's top is the last
-        row[n & (CH - 1)] = (e & 0xffffu) | (V << 16);
-        V += e >> 16;
+    if (fwd && gl) {
+      do {
+        if ((klen | plen) == 0) { done = true; break; }          // iterator.go:124-127
+        if (n == 0 && plen != 0) { st = LSMGPU_BLK_FIRST_PLEN; done = true; break; }
+        if (10 + plen > len) { st = LSMGPU_BLK_PREFIX_OOB; done = true; break; }
+        const uint32_t end = pos + 10 + klen + vlen;             // iterator.go:101-109
+        if (end > len) { st = LSMGPU_BLK_VALUE_OVERFLOW; done = true; break; }
+        row[n & (CH - 1)] = pos | (V << 16);
+        K += plen + klen;
+        V += vlen;
         n++;
-        di++;
+        pos = end;
         rec = true;
-        if (di == dn) {  // at the terminator, as the iterator
-          done = true;
-          pos = len - 13;
-          K += dk;
-        }
-      } else if (gl) {
-        do {
-          if ((klen | plen) == 0) { done = true; break; }          // iterator.go:124-127
-          if (n == 0 && plen != 0) { st = LSMGPU_BLK_FIRST_PLEN; done = true; break; }
-          if (10 + plen > len) { st = LSMGPU_BLK_PREFIX_OOB; done = true; break; }
-          const uint32_t end = pos + 10 + klen + vlen;             // iterator.go:101-109
-          if (end > len) { st = LSMGPU_BLK_VALUE_OVERFLOW; done = true; break; }
-          row[n & (CH - 1)] = pos | (V << 16);
-          K += plen + klen;
-          V += vlen;
-          n++;
-          pos = end;
-          rec = true;
-        } while (false);
-      }
+      } while (false);
     }
     if (!fwd && gl) {
       const uint32_t prev = __builtin_bswap32(x1);
@@ -2457,7 +2459,6 @@ __global__ void __launch_bounds__(2 * TB) wsc_walk_bidir_kernel(DecodeParams p) 
       } else if ((klen | plen) != 0 && by + 10 + klen + vlen == bx && 10 + plen <= len &&
                  (by != 0 || plen == 0)) {
         stk[bn] = by | (vlen << 16);
-        wave_lds_fence();
         bn++;
         bk += plen + klen;
         bx = by;
@@ -2484,6 +2485,33 @@ __global__ void __launch_bounds__(2 * TB) wsc_walk_bidir_kernel(DecodeParams p) 
       }
     }
   }
+  // a forward lane that met its partner takes the backward entries (ascending: the stack's top is
+  // the block's last entry) into its row, writing each full 32-record chunk out as it fills, and
+  // ends at the terminator as the iterator does
+  const uint32_t pbn = (uint32_t)__shfl((int)bn, (int)partner), pbk = (uint32_t)__shfl((int)bk, (int)partner);
+  wave_lds_fence();
+  if (fwd && met) {
+    uint32_t* const m0 = p.wmeta + (uint64_t)b * p.wcap;
+    for (uint32_t i = 0; i < pbn; i++) {
+      const uint32_t e = stk[pbn - 1 - i];
+      row[n & (CH - 1)] = (e & 0xffffu) | (V << 16);
+      V += e >> 16;
+      n++;
+      if ((n & (CH - 1)) == 0) {
+        uint4* d = reinterpret_cast<uint4*>(m0 + (n - CH));
+#pragma unroll
+        for (uint32_t q = 0; q < CH / 4; q++) d[q] = make_uint4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
+      }
+    }
+    K += pbk;
+    pos = len - 13;
+    done = true;
+  }
+#ifdef LSMGPU_DIAG
+  // (diagnostics: blocks whose walks met, in result[6]; the longest lane's steps, in result[7])
+  if (fwd && met && (p.ablate & 1024u)) atomicAdd(reinterpret_cast<unsigned long long*>(p.result + 6), 1ull);
+  if (lane == 0 && (p.ablate & 1024u)) atomicAdd(reinterpret_cast<unsigned long long*>(p.result + 7), (unsigned long long)steps);
+#endif
   const bool own = fwd && valid;  // the lane that reports the block
   if (own) row[n & (CH - 1)] = pos | (V << 16);  // the sentinel
   const uint64_t vm = __ballot(own);
@@ -2633,7 +2661,7 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 256>), dim3((nblk + 255) / 256), dim3(256), p.wpad, s, p);
   }
 #endif
-  else if (LSMGPU_KNOB(p.wlbidir, 0u) && !p.wfuse)  // a backward lane per block (batches of long blocks)
+  else if (LSMGPU_KNOB(p.wlbidir, 0u) && !p.wfuse && !LSMGPU_KNOB(p.weo, 0u))  // a backward lane per block
     hipLaunchKernelGGL(wsc_walk_bidir_kernel<128>, dim3((nblk + 127) / 128), dim3(256), 0, s, p);
 #ifdef LSMGPU_DIAG
   // fewer 256-block tiles than CUs (C5 2^30 B: 32 K blocks of 32 KiB, 128 tiles): smaller tiles

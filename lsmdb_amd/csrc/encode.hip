@@ -425,6 +425,139 @@ __global__ void __launch_bounds__(256) encode_pipe_kernel(EncodeParams p) {
   if (bad) atomicOr(p.flags, bad);
 }
 
+// encode_dense_kernel (blocks of large entries, > 128 B on average: C5's Zipf keys, C3): the
+// block's output as one run of 16-B pieces spread densely over the wave, as the copy's
+// copy_entries_dense_pipe does for the decode.  Entries 64 at a time, one per lane: offsets,
+// position, header fields; each entry counts its pieces -- the header piece (header + the key's
+// first 6 bytes, as encode_pipe_kernel writes it) when the key is >= 16 B, its key and value
+// pieces (16 B, the last overlapping back) -- and a wave scan gives each its first.  Then every
+// lane takes one piece of each 64-piece window: its entry found by LDS marks + a max-scan, the
+// next window's piece loaded before this window's store, every store a range-checked buffer
+// store over the table image.  Streams under 16 B (keys of 9-15 B and their headers, value
+// pointers' 15-B values) are written by the entry's lane in the plain order before the windows.
+__global__ void __launch_bounds__(256) encode_dense_kernel(EncodeParams p) {
+  __shared__ uint8_t s_mk[4][kWave];
+  const uint32_t lane = lane_id();
+  const uint32_t b = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+  uint8_t* const mk = s_mk[threadIdx.x >> 6];
+  EncBlock k;
+  if (!enc_block(p, b, lane, k)) return;
+  const uint64_t f = k.f, m = k.l - k.f, dl = k.dl;
+  const uint32_t lb = k.lb;
+  uint8_t* const out = k.out;
+  const __amdgpu_buffer_rsrc_t orsrc = buffer_rsrc(out, dl);
+  uint32_t bad = 0, bs = 0, carry = 0, tpos = 0, tend = 0;
+  struct Pc {
+    const uint8_t* src;
+    uint32_t dst;                  // kNoStore: none
+    uint32_t hdr, hprev;           // header piece: klen | vlen << 16, prev
+  };
+  for (uint64_t c0 = 0; c0 < m; c0 += kWave) {
+    const uint64_t r = c0 + lane;
+    const bool on = r < m;
+    const uint64_t e = f + (on ? r : m - 1);
+    const uint64_t ks = key_start(p, e), vs0 = vs_start(p, e), ke = p.key_end[e], ve = p.vs_end[e];
+    uint64_t sk = ks, sv = vs0;
+    if (p.src) {
+      const uint32_t si = p.src[e];
+      sk = si ? p.src_key_end[si - 1] : 0u;
+      sv = si ? p.src_vs_end[si - 1] : 0u;
+    }
+    const uint32_t klen = (uint32_t)(ke - ks), vlen = (uint32_t)(ve - vs0);
+    const uint32_t pos = k.position(e, ks, vs0);
+    if (c0 == 0) bs = readlane(pos, 0);
+    const uint32_t below = (uint32_t)__shfl_up((int)pos, 1u);
+    const uint32_t prev = r == 0 ? 0xffffffffu : (lane == 0 ? carry : below) - bs;  // builder.go:95-99
+    carry = readlane(pos, kWave - 1);
+    if (on) {
+      if (ke - ks <= 8 || ke - ks > 0xffff) bad |= 1;  // ParseKey needs len(key) > 8 (y.go:93-100)
+      if (ve - vs0 > 0xffff) bad |= 2;                  // header vlen is a uint16
+      if (r == m - 1) {
+        tpos = pos;
+        tend = pos + 10 + klen + vlen;
+      }
+      // short streams, plain: the header (8 + 2 B) and the key's pieces of a key under 16 B, the
+      // pieces of a value under 16 B
+      if (klen < 16) {
+        store_header(out + pos, klen, vlen, prev);
+        for (uint32_t q = 0; q < pieces16(klen); q++) copy_piece16(out + pos + 10, p.keys + sk, klen, q);
+      }
+      if (vlen < 16)
+        for (uint32_t q = 0; q < pieces16(vlen); q++) copy_piece16(out + pos + 10 + klen, p.vs + sv, vlen, q);
+    }
+    const uint32_t hp = on && klen >= 16 ? 1u : 0u, kp = on && klen >= 16 ? pieces16(klen) : 0u;
+    const uint32_t pc = hp + kp + (on && vlen >= 16 ? pieces16(vlen) : 0u);
+    const uint32_t ps = wave_scan_sat(pc, lane), ex = ps - pc;
+    const uint32_t T = __builtin_amdgcn_readlane(ps, 63);
+    uint32_t wcarry = 0;
+    auto win = [&](uint32_t r0) -> Pc {
+      mk[lane] = 0;
+      wave_lds_fence();
+      if (pc > 0 && ex >= r0 && ex < r0 + kWave) mk[ex - r0] = (uint8_t)(lane + 1);
+      wave_lds_fence();
+      const uint32_t own = max(wave_scan_max(mk[lane], lane), wcarry);  // 1 + the owner lane
+      wcarry = __builtin_amdgcn_readlane(own, 63);
+      wave_lds_fence();
+      const int L = (int)own - 1;
+      const uint32_t kv = (uint32_t)__shfl((int)(klen | (vlen << 16)), L);
+      const uint32_t posL = (uint32_t)__shfl((int)pos, L), prevL = (uint32_t)__shfl((int)prev, L);
+      const uint32_t exL = (uint32_t)__shfl((int)ex, L), hkL = (uint32_t)__shfl((int)(hp | (kp << 8)), L);
+      const uint64_t skL = (uint32_t)__shfl((int)sk, L), svL = (uint32_t)__shfl((int)sv, L);
+      const uint32_t kL = kv & 0xffffu, vL = kv >> 16, hL = hkL & 0xffu, kpL = hkL >> 8;
+      Pc c{p.pad, kNoStore, 0u, 0u};
+      const uint32_t P = r0 + lane;
+      if (P < T) {
+        const uint32_t q = P - exL;
+        if (q < hL) {  // the header piece: the key's first 16 B
+          c = Pc{p.keys + skL, posL, kv, prevL};
+        } else if (q < hL + kpL) {
+          const uint32_t o = min(16 * (q - hL), kL - 16);
+          c = Pc{p.keys + skL + o, posL + 10 + o, 0u, 0u};
+        } else {
+          const uint32_t o = min(16 * (q - hL - kpL), vL - 16);
+          c = Pc{p.vs + svL + o, posL + 10 + kL + o, 0u, 0u};
+        }
+      }
+      return c;
+    };
+    auto load = [&](const Pc& c) -> uint4 {
+      uint4 v;
+      __builtin_memcpy(&v, c.src, 16);
+      return v;
+    };
+    auto store = [&](const Pc& c, const uint4& v) {
+      const uint32_t kl = c.hdr & 0xffffu, vl = c.hdr >> 16, pr = c.hprev;
+      const u32x4 h = {bswap16(kl) << 16,                               // plen 00 00 | klen BE
+                       bswap16(vl) | (bswap16(pr >> 16) << 16),          // vlen BE | prev[31:16] BE
+                       bswap16(pr & 0xffffu) | (v.x << 16),              // prev[15:0] BE | key[0..1]
+                       (v.x >> 16) | (v.y << 16)};                       // key[2..5]
+      const u32x4 w = {v.x, v.y, v.z, v.w};
+      __builtin_amdgcn_raw_buffer_store_b128(c.hdr ? h : w, orsrc, c.dst, 0, 0);
+    };
+    Pc ca = win(0);
+    uint4 va = load(ca);
+    for (uint32_t r0 = 0; r0 < T; r0 += 2 * kWave) {  // two windows per trip: no register copy
+      const Pc cb = win(r0 + kWave);
+      const uint4 vb = load(cb);
+      store(ca, va);
+      if (r0 + kWave >= T) break;
+      ca = win(r0 + 2 * kWave);
+      va = load(ca);
+      store(cb, vb);
+    }
+  }
+  // terminator + restart (builder.go:121-123,146-160), by the lane of the block's last entry
+  if (lane == (uint32_t)((m - 1) & (kWave - 1))) {
+    uint8_t* t = out + tend;
+    store_header(t, 0, 3, tpos - bs);
+    t[10] = 0;
+    t[11] = 0;
+    t[12] = 0;
+    store_be32(out + dl + 4ull * lb, tend + 13);
+  }
+  if (bad) atomicOr(p.flags, bad);
+}
+
 // Builder.ReachedCapacity (builder.go:140-143) as compactBuildTables applies it before every
 // Add (levels.go:265-271): a table holding e entries [s, s + e) is closed when
 //   10e + K + V + 13 fb + 8 + 4 fb + 8 > cap,   fb = (e - 1) / epb finished blocks
@@ -542,6 +675,17 @@ hipError_t launch_encode(const EncodeParams& p0, int num_cus, hipStream_t s) {
   p.pipe = 2u;
   // J = lanes per entry ~ the average entry's 16-B pieces (C2: 129 B -> 8; C3: ~1.1 KB -> 64)
   const uint64_t avg = p.n ? (p.key_total + p.vs_total) / p.n : 120;
+  // blocks of > 128-B entries: encode_dense_kernel (same box, C5 encode 0.560-0.562 -> 0.489-0.490
+  // ms, C3 0.448-0.460 -> 0.430-0.442, profiles/r06ab); diag build: LSMGPU_ENC_DENSE=0 keeps the
+  // J-lane passes; the LSMGPU_ENC_J test hook selects those too
+  p.dense = 1u;
+#ifdef LSMGPU_DIAG
+  if (const char* de = getenv("LSMGPU_ENC_DENSE")) p.dense = atoi(de) != 0;
+#endif
+  if (LSMGPU_KNOB(p.dense, 1u) && avg > 128 && !getenv("LSMGPU_ENC_J")) {
+    hipLaunchKernelGGL(encode_dense_kernel, dim3((p.nblocks + 3) / 4), dim3(256), 0, s, p);
+    return hipGetLastError();
+  }
   // LSMGPU_ENC_J (test hook): one of the compiled J (4, 8, 16) whatever the entry size
   if (const char* je = getenv("LSMGPU_ENC_J")) {
     const int jj = atoi(je);

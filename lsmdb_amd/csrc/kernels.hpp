@@ -126,6 +126,7 @@ struct EncodeParams {
   const uint32_t* src_vs_end;
   uint32_t hdr16;  // set by launch_encode: header + the key's first 6 bytes as one 16-B store
   const uint8_t* pad;  // 16 readable device bytes: the source of loads no piece uses
+  uint32_t dense;  // set by launch_encode: encode_dense_kernel for blocks of large entries
   uint32_t pipe;   // set by launch_encode: encode_pipe_kernel (next pass's first pieces loaded
                    // before this pass's stores)
 };

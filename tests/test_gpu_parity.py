@@ -606,6 +606,28 @@ def test_encode_template_instances(codec, oracle, monkeypatch, knob, val):
         assert out == ref, f"{knob}={val} cfg={cfg} epb={epb}"
 
 
+def test_encode_dense_kernel(codec, oracle, monkeypatch):
+    """encode_dense_kernel (64-piece windows over a block's entries, header pieces carrying the
+    header fields, short streams in the plain order) bit-exact against the oracle Builder on
+    blocks of > 128-B entries: C3, C5, 100 / 180 entries per block, and random 9-300-B keys with
+    3-60-B values (short keys, short values)."""
+    if DIAG:
+        monkeypatch.setenv("LSMGPU_ENC_DENSE", "1")
+    cases = []
+    for cfg, n, epb in [(3, 4000, None), (5, 20000, None), (5, 20000, 100), (3, 3000, 180)]:
+        c = _cols(cfg, n, seed=n + 5)
+        cases.append(((c.keys, c.key_end, c.vs, c.vs_end),
+                      c.entries_per_block if epb is None else epb,
+                      c.block_bytes if epb is None else 0))
+    cases.append((_random_cols(20000, 53, kmin=9, kmax=300, vmin=3, vmax=60), 0, 4096))
+    cases.append((_random_cols(20000, 59, kmin=9, kmax=300, vmin=3, vmax=400), 70, 0))
+    for cols, e, bb in cases:
+        ref, ref_dl, ref_rs = oracle.build_cols(*cols, e, bb)
+        out, dl, rs = codec.encode_host(*cols, e, bb)
+        assert dl == ref_dl and np.array_equal(rs, ref_rs)
+        assert out == ref, f"dense epb={e} bb={bb}"
+
+
 @pytest.mark.skipif(not DIAG, reason="LSMGPU_ENC_PIPE: diagnostic build only")
 @pytest.mark.parametrize("pipe", ["1", "2"])
 @pytest.mark.parametrize("j", ["4", "8", "16"])
