@@ -486,7 +486,8 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     p.wdmax = 0xffffffffu;
     p.wdmin = 128u;
     p.wpdepth = 3u;
-    p.wlbidir = 0u;
+    // lane walks over blocks above 8 KiB: a second lane per block walks it backward
+    p.wlbidir = max_blk_len > 8192 ? 1u : 0u;
 #ifdef LSMGPU_DIAG
     decode_diag_knobs(p, nblk, cus, max_blk_len, wk_env);
     // group walks: the copy in the walk's launch (LSMGPU_WSC_COPYFUSE=1), by workgroups past the

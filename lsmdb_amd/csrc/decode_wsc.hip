@@ -2321,24 +2321,15 @@ __global__ void __launch_bounds__(TB) wsc_walk_persist_kernel(DecodeParams p) {
 // iterator's.  Records, flushes, tile scan, look-back and epilogue are the lane walk's.
 constexpr uint32_t kBackCap = 96;  // backward entries per block (LDS stack)
 
-// header bytes [0, 8): plen klen vlen (no wait: the caller waits once for every direction)
-__device__ __forceinline__ void load_hdr_nt(const uint8_t* g, uint32_t& w0, uint32_t& w1) {
-  typedef unsigned int v2 __attribute__((ext_vector_type(2)));
-  v2 a;
-  asm volatile("global_load_dwordx2 %0, %1, off nt" : "=v"(a) : "v"(g) : "memory");
-  w0 = a.x;
-  w1 = a.y;
+// non-temporal header reads the compiler sees (so it places one wait for both directions'
+// loads before their first use): 8 B at g, or the 16 B at g (any alignment)
+typedef uint32_t u32x2u __attribute__((ext_vector_type(2), aligned(1)));
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+__device__ __forceinline__ u32x2u ld8_nt(const uint8_t* g) {
+  return __builtin_nontemporal_load(reinterpret_cast<const u32x2u*>(g));
 }
-// the 16 B at g (a header at g + 6: plen, klen, vlen, prev in bytes 6-15)
-__device__ __forceinline__ void load_hdr16_nt(const uint8_t* g, uint32_t& w0, uint32_t& w1,
-                                              uint32_t& w2, uint32_t& w3) {
-  typedef unsigned int v4 __attribute__((ext_vector_type(4)));
-  v4 a;
-  asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(a) : "v"(g) : "memory");
-  w0 = a.x;
-  w1 = a.y;
-  w2 = a.z;
-  w3 = a.w;
+__device__ __forceinline__ u32x4u ld16_nt(const uint8_t* g) {
+  return __builtin_nontemporal_load(reinterpret_cast<const u32x4u*>(g));
 }
 
 template <uint32_t TB>
@@ -2422,14 +2413,22 @@ __global__ void __launch_bounds__(2 * TB) wsc_walk_bidir_kernel(DecodeParams p) 
       else if (bstart && (by > bx || bx - by < 10 || by <= s_pos || by < 6)) bact = false;
       else { gl = true; ga = bstart ? by : bx; }
     }
-    // one load instruction for the wave: every lane the 16 B ending with its header (bytes 6-15:
-    // plen, klen, vlen, prev; the entry is inside the block, so the read is); the header at 0
-    // (every forward lane's first step) as 8 B of its own
+    // one load instruction for the wave: every lane reads the 16 B that end with its header
+    // (bytes 6-15: plen, klen, vlen, prev), inside the block; a header at 0 (a forward lane's
+    // first step) from the block's first 16 B, or, in a block under 16 B, as 8 B of its own
     uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
     const bool at0 = ga < 6;
-    if (gl && !at0) load_hdr16_nt(blk + ga - 6, w0, w1, w2, w3);
-    if (gl && at0) load_hdr_nt(blk + ga, w0, w1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (one round trip for both directions)
+    if (gl && (!at0 || len >= 16)) {
+      const u32x4u v = ld16_nt(blk + (at0 ? 0u : ga - 6));
+      w0 = v.x;
+      w1 = v.y;
+      w2 = v.z;
+      w3 = v.w;
+    } else if (gl) {
+      const u32x2u v = ld8_nt(blk + ga);
+      w0 = v.x;
+      w1 = v.y;
+    }
     const uint32_t plen = at0 ? __builtin_amdgcn_perm(0u, w0, 0x0c0c0001u) : __builtin_amdgcn_perm(0u, w1, 0x0c0c0203u);
     const uint32_t klen = at0 ? __builtin_amdgcn_perm(0u, w0, 0x0c0c0203u) : __builtin_amdgcn_perm(0u, w2, 0x0c0c0001u);
     const uint32_t vlen = at0 ? __builtin_amdgcn_perm(0u, w1, 0x0c0c0001u) : __builtin_amdgcn_perm(0u, w2, 0x0c0c0203u);
@@ -2661,7 +2660,9 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
     hipLaunchKernelGGL((wsc_walk_kernel<kWalkLane, 256>), dim3((nblk + 255) / 256), dim3(256), p.wpad, s, p);
   }
 #endif
-  else if (LSMGPU_KNOB(p.wlbidir, 0u) && !p.wfuse && !LSMGPU_KNOB(p.weo, 0u))  // a backward lane per block
+  // a backward lane per block (batches of long blocks: C5 walk 0.183-0.185 -> 0.170-0.172 ms,
+  // decode 1,529-1,536 -> 1,557-1,564 GiB/s, view 0.213 -> 0.199 ms, profiles/r06ai)
+  else if (p.wlbidir && !p.wfuse && !LSMGPU_KNOB(p.weo, 0u))
     hipLaunchKernelGGL(wsc_walk_bidir_kernel<128>, dim3((nblk + 127) / 128), dim3(256), 0, s, p);
 #ifdef LSMGPU_DIAG
   // fewer 256-block tiles than CUs (C5 2^30 B: 32 K blocks of 32 KiB, 128 tiles): smaller tiles

@@ -1,7 +1,7 @@
 # the lane walk with a backward lane per block (diag, LSMGPU_WSC_LBIDIR=1): parity with the lane
 # walk forced, then C5 and the compaction replay's decode (48 K blocks of 100 entries)
 set -o pipefail
-O=gpurun_out/${OUT:-r06ag}
+O=gpurun_out/${OUT:-r06ai}
 mkdir -p $O
 LSMGPU_LIB_VARIANT=diag LSMGPU_WSC_WALK=lane LSMGPU_WSC_LBIDIR=1 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
   tests/test_gpu_parity.py tests/test_gpu_golden.py -k "not kernel_times" > $O/parity.log 2>&1 || { tail -40 $O/parity.log; exit 1; }

@@ -170,6 +170,71 @@ def test_prefix_compressed_random(codec, oracle):
     _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln))
 
 
+@pytest.mark.parametrize("shape", ["c5", "prefix", "bogus_prev"])
+def test_lane_walk_backward(codec, oracle, monkeypatch, shape):
+    """The lane walk over blocks above 8 KiB runs a second lane per block backward along the
+    headers' prev fields (wsc_walk_bidir_kernel); forced here on batches the group walk would
+    take.  c5: Builder blocks of ~150 Zipf entries (the chains meet); prefix: hand-built blocks of
+    > 8 KiB with prefix-compressed entries (plen > 0 after the first: the backward key bytes
+    include plen); bogus_prev: Builder blocks whose prev fields were overwritten at random (a
+    backward lane stops at the first entry that does not end where the last accepted one starts;
+    the result stays the forward iterator's)."""
+    import struct
+    monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
+    monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
+    rng = np.random.default_rng(61)
+    if shape in ("c5", "bogus_prev"):
+        c = _cols(5, 30000, seed=67)
+        ref, _, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, c.entries_per_block, c.block_bytes)
+        off, ln, _, _ = oracle.parse_index(ref + b"{}" + (2).to_bytes(4, "big"))
+        data = bytearray(ref)
+        if shape == "bogus_prev":
+            for b in range(0, off.size, 2):  # every other block: ten random prev fields, some 0
+                o, L = int(off[b]), int(ln[b])
+                pos, starts = 0, []
+                while pos < L - 13:
+                    pl, kl, vl = struct.unpack(">HHH", data[o + pos: o + pos + 6])
+                    starts.append(pos)
+                    pos += 10 + kl + vl
+                starts.append(L - 13)
+                for i in rng.choice(len(starts), 10, replace=False):
+                    v = 0 if rng.random() < 0.3 else int(rng.integers(0, L))
+                    data[o + starts[i] + 6: o + starts[i] + 10] = v.to_bytes(4, "big")
+        data = bytes(data)
+    else:
+        data = bytearray()
+        offs, lens = [], []
+        for b in range(120):
+            blk = bytearray()
+            base = bytes(rng.integers(0, 256, int(rng.integers(9, 40)), dtype=np.uint8))
+            prev = 0xFFFFFFFF
+            while len(blk) < 9000 + int(rng.integers(0, 20000)):
+                pos = len(blk)
+                if pos == 0:
+                    plen, diff = 0, base
+                else:
+                    plen = int(rng.integers(0, len(base) + 5))
+                    diff = bytes(rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8))
+                    if plen == 0 and not diff:
+                        diff = b"x"
+                val = bytes(rng.integers(0, 256, int(rng.integers(0, 200)), dtype=np.uint8))
+                blk += struct.pack(">HHHI", plen, len(diff), len(val), prev) + diff + val
+                prev = pos
+            blk += struct.pack(">HHHI", 0, 0, 3, prev) + b"\0\0\0"
+            offs.append(len(data))
+            lens.append(len(blk))
+            data += blk
+        data = bytes(data)
+        off, ln = np.array(offs, np.uint32), np.array(lens, np.uint32)
+    from lsmdb_amd.codec import MODE_VIEW
+    assert int(ln.max()) > 8192
+    o = oracle.decode(data, off, ln)
+    _assert_same(codec.decode_host(data, off, ln), o)
+    g = codec.decode_host(data, off, ln, mode=MODE_VIEW)
+    assert g.n_entries == o.n_entries and np.array_equal(g.view, o.view)
+    assert np.array_equal(g.blk_first, o.blk_first) and np.array_equal(g.blk_status, o.blk_status)
+
+
 def test_device_resident_async(codec, oracle):
     """The benchmarked entry point (all pointers on device) on a C2 table."""
     import torch
