@@ -364,6 +364,7 @@ static void decode_diag_knobs(DecodeParams& p, uint64_t nblk, uint64_t cus, uint
   if (const char* v = env("LSMGPU_WSC_DMAX")) p.wdmax = (uint32_t)atoi(v);
   if (const char* v = env("LSMGPU_WSC_DMIN")) p.wdmin = (uint32_t)atoi(v);
   if (const char* v = env("LSMGPU_WSC_LBIDIR")) p.wlbidir = atoi(v) == 0 ? 0u : 1u;
+  if (const char* v = env("LSMGPU_WSC_B16")) p.wb16 = atoi(v) == 0 ? 0u : 1u;
   if (const char* v = env("LSMGPU_WSC_PDEPTH")) p.wpdepth = (uint32_t)std::min(std::max(atoi(v), 2), 4);
   const char* sl = env("LSMGPU_WSC_SLOT");
   p.wslot = sl && sl[0] == 's' ? 1u : (sl && sl[0] == 'n' ? 2u : 0u);
@@ -488,6 +489,7 @@ int lsmgpu_decode_blocks_async(lsmgpu_ctx* c, const uint8_t* d_data, uint64_t da
     p.wpdepth = 3u;
     // lane walks over blocks above 8 KiB: a second lane per block walks it backward
     p.wlbidir = max_blk_len > 8192 ? 1u : 0u;
+    p.wb16 = 0u;
 #ifdef LSMGPU_DIAG
     decode_diag_knobs(p, nblk, cus, max_blk_len, wk_env);
     // group walks: the copy in the walk's launch (LSMGPU_WSC_COPYFUSE=1), by workgroups past the

@@ -178,7 +178,7 @@ __device__ __forceinline__ void lds_st(uint32_t* a, uint32_t v) {
 
 template <uint32_t L>
 __device__ __forceinline__ void bidir_bwd(const uint8_t* blk, uint32_t len, uint32_t* bst,
-                                          BiState* st, uint32_t k, uint32_t gb) {
+                                          BiState* st, uint32_t k, uint32_t gb, bool b16) {
   constexpr uint64_t kMask = (1ull << L) - 1;
   if (len < 23) return;
   uint32_t tp, tk, tv;
@@ -195,7 +195,15 @@ __device__ __forceinline__ void bidir_bwd(const uint8_t* blk, uint32_t len, uint
     const bool act = (uint64_t)k * bstride <= bnext;
     const uint32_t q = bnext - k * bstride;
     uint32_t plen = 1, klen = 0, vlen = 0, prv = kBiNone;
-    if (act && q + 10 <= len) {
+    if (act && q + 10 <= len && q >= 6 && b16) {
+      // one load: the 16 B ending with the header (bytes 6-15: plen, klen, vlen, prev)
+      uint4 w;
+      __builtin_memcpy(&w, blk + q - 6, 16);
+      plen = __builtin_amdgcn_perm(0u, w.y, 0x0c0c0203u);
+      klen = __builtin_amdgcn_perm(0u, w.z, 0x0c0c0001u);
+      vlen = __builtin_amdgcn_perm(0u, w.z, 0x0c0c0203u);
+      prv = __builtin_bswap32(w.w);
+    } else if (act && q + 10 <= len) {
       uint2 w;
       __builtin_memcpy(&w, blk + q, 8);
       uint16_t lo;
@@ -618,7 +626,7 @@ __global__ void __launch_bounds__(MODE == kWalkGroup || MODE == kWalkGroupBi || 
           }
         }
         if constexpr (BI) {
-          if (bw) bidir_bwd<L>(blk, len, s_bstack[g], &s_bi[g], k, gb);
+          if (bw) bidir_bwd<L>(blk, len, s_bstack[g], &s_bi[g], k, gb, LSMGPU_KNOB(p.wb16, 0u) != 0);
           else bidir_fwd<L>(p, blk, len, meta, row, s_bstack[g], &s_bi[g], k, gb, pos, gn, gK, gV, gst);
         } else {
         uint32_t kref = 0xffffffffu, vref = 0, stride = 0;  // no shape yet: round 1 takes one

@@ -95,6 +95,7 @@ struct DecodeParams {
   uint32_t wdmin;           // (diag) copy: the dense mapping above this average entry (128)
   uint32_t wpdepth;         // (diag) copy_entries_pipe: entry groups in flight + 1 (3)
   uint32_t wlbidir;         // lane walk: a second lane per block walking backward (blocks > 8 KiB)
+  uint32_t wb16;            // (diag) group walk's backward reads: one 16-B load per header
 
 };
 
