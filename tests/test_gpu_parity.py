@@ -170,7 +170,7 @@ def test_prefix_compressed_random(codec, oracle):
     _assert_same(codec.decode_host(data, off, ln), oracle.decode(data, off, ln))
 
 
-@pytest.mark.parametrize("shape", ["c5", "prefix", "bogus_prev"])
+@pytest.mark.parametrize("shape", ["c5", "prefix", "bogus_prev", "bad_len"])
 def test_lane_walk_backward(codec, oracle, monkeypatch, shape):
     """The lane walk over blocks above 8 KiB runs a second lane per block backward along the
     headers' prev fields (wsc_walk_bidir_kernel); forced here on batches the group walk would
@@ -178,16 +178,27 @@ def test_lane_walk_backward(codec, oracle, monkeypatch, shape):
     > 8 KiB with prefix-compressed entries (plen > 0 after the first: the backward key bytes
     include plen); bogus_prev: Builder blocks whose prev fields were overwritten at random (a
     backward lane stops at the first entry that does not end where the last accepted one starts;
-    the result stays the forward iterator's)."""
+    the result stays the forward iterator's); bad_len: Builder blocks with a random klen or vlen
+    in the middle (the forward walk errors there or runs off the chain, and must not meet)."""
     import struct
     monkeypatch.setenv("LSMGPU_DECODE_PATH", "wsc")
     monkeypatch.setenv("LSMGPU_WSC_WALK", "lane")
     rng = np.random.default_rng(61)
-    if shape in ("c5", "bogus_prev"):
+    if shape in ("c5", "bogus_prev", "bad_len"):
         c = _cols(5, 30000, seed=67)
         ref, _, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, c.entries_per_block, c.block_bytes)
         off, ln, _, _ = oracle.parse_index(ref + b"{}" + (2).to_bytes(4, "big"))
         data = bytearray(ref)
+        if shape == "bad_len":
+            for b in range(0, off.size, 3):  # every third block: one length field in the middle
+                o, L = int(off[b]), int(ln[b])
+                pos, starts = 0, []
+                while pos < L - 13:
+                    pl, kl, vl = struct.unpack(">HHH", data[o + pos: o + pos + 6])
+                    starts.append(pos)
+                    pos += 10 + kl + vl
+                at = starts[len(starts) // 2] + (2 if rng.random() < 0.5 else 4)
+                data[o + at: o + at + 2] = int(rng.integers(0, 65536)).to_bytes(2, "big")
         if shape == "bogus_prev":
             for b in range(0, off.size, 2):  # every other block: ten random prev fields, some 0
                 o, L = int(off[b]), int(ln[b])
