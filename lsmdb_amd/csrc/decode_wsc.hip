@@ -2616,6 +2616,7 @@ hipError_t launch_decode_wsc(const DecodeParams& p, hipStream_t s, hipEvent_t mi
   //   materialize, wide tiles (> 4 x 256-block tiles per CU): two 576-thread tiles per workgroup
   //   view-only fused into the walk: kWalkLaneView, 576- or 256-block tiles
   //   <= 64 blocks per CU: 8 lanes forward + 8 backward per block (kWalkGroupBi)
+  //   blocks above 8 KiB: one lane forward + one backward per block (wsc_walk_bidir_kernel)
   //   otherwise one lane per block, 256-block tiles
   const bool persist = LSMGPU_KNOB(p.wpersist, 1u) && !p.wfuse && p.wwalk != kWalkGroup && p.wwide == 576 &&
                        LSMGPU_KNOB(p.wchunk, 32u) == 32 && !LSMGPU_KNOB(p.weo, 0u);

@@ -367,6 +367,34 @@ def test_pieces_at_data_end(codec, oracle, monkeypatch, last):
     assert np.array_equal(bufs.val_end[:n].cpu().numpy().view(np.uint32), o.val_end)
 
 
+def test_large_batch_of_long_blocks(codec, oracle):
+    """A device-resident batch of > 64 blocks per CU of 100-entry blocks (C1 / C4 shape, 17 K
+    blocks): the copy pipelines blocks of >= 64 entries through record windows, two waves per
+    block (copy_entries_pipe with wpipe = 2), checked against the oracle on every output."""
+    import torch
+    c = _cols(1, 1_750_000, seed=71)
+    ref, _, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, 100, 0)
+    sst = ref + b"{}" + (2).to_bytes(4, "big")
+    off, ln, _, _ = oracle.parse_index(sst)
+    assert off.size > 64 * 256
+    o = oracle.decode(sst, off, ln)
+    dev = torch.device("cuda", 0)
+    d_data = torch.from_numpy(np.frombuffer(sst, np.uint8).copy()).to(dev)
+    d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+    d_len = torch.from_numpy(ln.view(np.int32)).to(dev)
+    bufs = codec.alloc_decode(len(sst), int(ln.sum()), off.size, 1, ent_cap=o.n_entries)
+    codec.decode_device_async(d_data, d_off, d_len, int(ln.max()), 1, bufs)
+    codec.synchronize()
+    res = bufs.result.cpu().numpy()
+    n = o.n_entries
+    assert res[0] == n and res[5] == 0
+    assert bufs.key_data[: int(res[1])].cpu().numpy().tobytes() == o.key_data.tobytes()
+    assert bufs.val_data[: int(res[2])].cpu().numpy().tobytes() == o.val_data.tobytes()
+    assert np.array_equal(bufs.key_end[:n].cpu().numpy().view(np.uint32), o.key_end)
+    assert np.array_equal(bufs.val_end[:n].cpu().numpy().view(np.uint32), o.val_end)
+    assert np.array_equal(bufs.blk_first.cpu().numpy().view(np.uint32), o.blk_first)
+
+
 def test_capacity_overflow_reported(codec, oracle):
     c = _cols(1, 1000, seed=4)
     ref, _, _ = oracle.build_cols(c.keys, c.key_end, c.vs, c.vs_end, 100, 0)
