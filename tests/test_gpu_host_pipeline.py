@@ -115,7 +115,9 @@ def test_host_register_shared_pages(codec, mixed, monkeypatch):
     """Two non-page-aligned copies of the input in one allocation, 16 B apart (a page shared by
     both, as Go heap buffers under LoadToRAM share pages, table/table.go:117-123,329-338): both
     registered, both decoded, the first unregistered and the second decoded again, then
-    unregistered, then the first decoded unregistered."""
+    unregistered, then the first decoded unregistered.  (Since ABI 4 registration is bookkeeping
+    only -- nothing is page-locked -- so this checks that the registry's ranges, not pages,
+    decide what is registered.)"""
     monkeypatch.setenv("LSMGPU_HOST_CHUNK", "1048576")
     data, off, ln, ref = mixed
     n = len(data)
@@ -150,9 +152,9 @@ def test_host_register_cycles_and_nesting(codec, mixed, monkeypatch):
         _check(codec.decode_host(sub, off, ln), ref, 3, "cycle")
         codec.host_unregister(sub)
     codec.host_register(buf)
-    codec.host_register(sub)  # nested: every page already pinned
+    codec.host_register(sub)  # nested inside a registered range
     _check(codec.decode_host(sub, off, ln), ref, 3, "nested")
-    codec.host_unregister(buf)  # the outer range goes first: sub keeps its pages
+    codec.host_unregister(buf)  # the outer range goes first: sub stays registered
     _check(codec.decode_host(sub, off, ln), ref, 3, "nested, outer unpinned")
     codec.host_unregister(sub)
     rc = _lib.lib().lsmgpu_host_unregister(codec._ctx, _ptr(sub))
