@@ -1,4 +1,5 @@
 # the copy pipeline's key and value stores through one resource (diag, LSMGPU_WSC_KV1): parity, C2
+# (the knob was removed with the variant after this measurement; the script is the record of profiles/r06am)
 set -o pipefail
 O=gpurun_out/${OUT:-r06am}
 mkdir -p $O
